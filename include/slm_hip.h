@@ -1,0 +1,124 @@
+/*
+ * slm_hip.h — C-ABI of libslm_hip.so, the MI355X (gfx950) hot path of the
+ * Gerchberg–Saxton / gradient-descent hologram loops.
+ *
+ * Reference interfaces replaced (pranislav/Spatial_Light_Modulator_Module,
+ * snapshot 2024-10-08; the reference is pure Python and has no FFI, so these
+ * are the entry points a ctypes binding of that path binds — see
+ * INTEGRATION.md):
+ *   slm_gs / slm_plan_* with SLM_ALGO_GS  -> gerchberg_saxton(demanded_output, args)
+ *                                            src/algorithms.py:10-49
+ *   slm_gd / slm_plan_* with SLM_ALGO_GD  -> gradient_descent(demanded_output, args)
+ *                                            src/algorithms.py:60-112 (+ error_f :161,
+ *                                            dEdX_complex :179, make_initial_guess
+ *                                            "fourier" :153-156)
+ *   slm_fft2                              -> scipy.fft.fft2 / ifft2 as called at
+ *                                            src/algorithms.py:27,31,34,84,88 (unscaled)
+ *   slm_comm_* / slm_plan_gather_phase    -> no reference counterpart: the batch
+ *                                            loop of src/generate_hologram_sequence.py:19-31
+ *                                            sharded over GPUs, phases gathered over RCCL.
+ *
+ * Conventions: plain pointers and sizes, C-contiguous row-major host arrays,
+ * complex values interleaved (re, im) float32. The caller owns host buffers;
+ * the library owns device buffers. Every function returns 0 on success or a
+ * negative code; slm_last_error() describes the last failure of the calling
+ * thread. Nothing here falls back to the CPU: without a usable gfx950 device
+ * every compute entry point fails.
+ */
+#ifndef SLM_HIP_H
+#define SLM_HIP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SLM_ALGO_GS 0
+#define SLM_ALGO_GD 1
+
+#define SLM_TGT_U8 0  /* uint8 target; amplitude = float16(sqrt(T)) as numpy does */
+#define SLM_TGT_F32 1 /* float32 target; amplitude = sqrtf(T) */
+
+/* kernel classes for timing / roofline queries */
+#define SLM_KERNEL_COL_MAIN 0 /* GS column pass, or GD gradient column pass */
+#define SLM_KERNEL_ROW_MAIN 1 /* GS / GD fused row pass */
+#define SLM_KERNEL_GD_STATS 2 /* GD statistics column pass */
+#define SLM_KERNEL_OTHER 3    /* setup, phase extraction, reductions */
+#define SLM_NUM_KERNEL_CLASSES 4
+
+#define SLM_ERR_ARG (-1)
+#define SLM_ERR_HIP (-2)
+#define SLM_ERR_UNSUPPORTED (-3)
+#define SLM_ERR_STATE (-4)
+#define SLM_ERR_COMM (-5)
+
+typedef struct slm_plan slm_plan;
+
+/* ---- library ---------------------------------------------------------- */
+int slm_init(int device);            /* select the GPU of this process */
+int slm_device_count(void);
+const char* slm_last_error(void);
+const char* slm_version(void);
+int slm_supported_length(int n);    /* 1 if n is a supported row/column length */
+
+/* ---- plans: device-resident batches ------------------------------------
+ * A plan holds `batch` holograms of height x width on the current device.
+ * Upload once, run many times (bench), read results.                       */
+int slm_plan_create(int algo, int batch, int height, int width, int tgt_type, int has_ain, int max_loops,
+                    slm_plan** out);
+int slm_plan_destroy(slm_plan* plan);
+/* targets [batch][height][width] of tgt_type; norm = max(T) and sum(T^2) are
+ * reduced on the device */
+int slm_plan_set_target(slm_plan* plan, const void* tgt);
+int slm_plan_set_ain(slm_plan* plan, const float* ain);           /* [height][width] sqrt(incoming intensity) */
+int slm_plan_set_phase(slm_plan* plan, const float* phase);       /* GS warm start [batch][h][w]; NULL = cold */
+int slm_plan_set_field(slm_plan* plan, const float* field_re_im); /* GD initial x [batch][h][w][2]; NULL = fourier */
+int slm_plan_set_lr(slm_plan* plan, const float* lr);             /* GD learning rate per iteration [max_loops] */
+/* Enqueue one full run (setup + loops iterations + outputs) on the plan's
+ * stream. tol as in `while error > tolerance`; checked != 0 evaluates that
+ * test on the device after every iteration (required when tol > 0). */
+int slm_plan_run(slm_plan* plan, int loops, double tol, int checked, float white_attention);
+/* As slm_plan_run, additionally timing every launch with HIP events on the
+ * plan's stream; accumulates microseconds and launch counts per kernel class. */
+int slm_plan_run_timed(slm_plan* plan, int loops, double tol, int checked, float white_attention,
+                       double* us_per_class, int* launches_per_class);
+int slm_plan_sync(slm_plan* plan);
+/* phase [batch][h][w] float32 (radians, angle convention of np.angle);
+ * expected [batch][h][w] float32 = |C|^2 of the last iteration (scale by
+ * norm / stats[..][0] for expected_outcome); stats [batch][max_loops][4] =
+ * (max E, sum E^2, sum E T, error); iters [batch] iterations executed.
+ * Any pointer may be NULL. */
+int slm_plan_read(slm_plan* plan, float* phase, float* expected, double* stats, int* iters);
+/* norm [batch] and sum T^2 [batch] as reduced on the device */
+int slm_plan_read_target_stats(slm_plan* plan, double* norm, double* sum_t2);
+/* algorithmic HBM bytes moved by one launch of a kernel class */
+long long slm_plan_kernel_bytes(slm_plan* plan, int kernel_class);
+/* info[0] = column tile width, info[1] = column workgroups per hologram,
+ * info[2] = column threads, info[3] = row threads, info[4] = rows per workgroup */
+int slm_plan_info(slm_plan* plan, int* info);
+
+/* ---- one-shot helpers (upload, run, read) ------------------------------ */
+int slm_gs(const void* tgt, int tgt_type, const float* ain, int batch, int height, int width, int max_loops,
+           double tol, const float* init_phase, float* out_phase, float* out_expected, double* out_stats,
+           int* out_iters);
+int slm_gd(const void* tgt, int tgt_type, const float* ain, int batch, int height, int width, int max_loops,
+           double tol, const float* init_field, const float* lr, float white_attention, float* out_phase,
+           float* out_expected, double* out_stats, int* out_iters);
+
+/* unscaled 2-D C2C transform of [batch][h][w] complex64 (test entry) */
+int slm_fft2(const float* in_re_im, float* out_re_im, int batch, int height, int width, int inverse);
+
+/* ---- multi-GPU (one process per GPU, RCCL over xGMI) ------------------- */
+int slm_comm_unique_id(unsigned char* id128);
+int slm_comm_init(int nranks, int rank, const unsigned char* id128);
+int slm_comm_destroy(void);
+/* Gather every rank's phase output to `root`: rank r contributes its plan's
+ * batch (counts[r] holograms, same h x w everywhere); on root, host_out
+ * receives sum(counts) x h x w float32 in rank order (may be NULL to leave
+ * the gathered array on the device). Collective; enqueued on the plan stream
+ * and synchronised before returning. */
+int slm_plan_gather_phase(slm_plan* plan, const int* counts, int root, float* host_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SLM_HIP_H */

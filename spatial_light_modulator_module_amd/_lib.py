@@ -1,0 +1,259 @@
+"""ctypes binding of libslm_hip.so (C-ABI declared in include/slm_hip.h).
+
+The shared library is the only compute path of this package: there is no CPU
+fallback. Loading fails loudly when the library has not been built, and every
+compute call raises :class:`SlmError` when no gfx950 device is usable.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libslm_hip.so")
+
+ALGO_GS = 0
+ALGO_GD = 1
+TGT_U8 = 0
+TGT_F32 = 1
+
+KERNEL_COL_MAIN = 0
+KERNEL_ROW_MAIN = 1
+KERNEL_GD_STATS = 2
+KERNEL_OTHER = 3
+NUM_KERNEL_CLASSES = 4
+KERNEL_CLASS_NAMES = ("col_main", "row_main", "gd_stats", "other")
+
+SUPPORTED_LENGTHS = (64, 128, 256, 512, 768, 1024, 2048, 4096)
+
+
+class SlmError(RuntimeError):
+    """A libslm_hip call failed (message from slm_last_error)."""
+
+
+_c_int = ctypes.c_int
+_c_double = ctypes.c_double
+_c_float = ctypes.c_float
+_vp = ctypes.c_void_p
+_P = ctypes.POINTER
+
+# (name, restype, argtypes) for every symbol of include/slm_hip.h
+_SIGNATURES = [
+    ("slm_init", _c_int, [_c_int]),
+    ("slm_device_count", _c_int, []),
+    ("slm_last_error", ctypes.c_char_p, []),
+    ("slm_version", ctypes.c_char_p, []),
+    ("slm_supported_length", _c_int, [_c_int]),
+    ("slm_plan_create", _c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _P(_vp)]),
+    ("slm_plan_destroy", _c_int, [_vp]),
+    ("slm_plan_set_target", _c_int, [_vp, _vp]),
+    ("slm_plan_set_ain", _c_int, [_vp, _vp]),
+    ("slm_plan_set_phase", _c_int, [_vp, _vp]),
+    ("slm_plan_set_field", _c_int, [_vp, _vp]),
+    ("slm_plan_set_lr", _c_int, [_vp, _vp]),
+    ("slm_plan_run", _c_int, [_vp, _c_int, _c_double, _c_int, _c_float]),
+    ("slm_plan_run_timed", _c_int, [_vp, _c_int, _c_double, _c_int, _c_float, _vp, _vp]),
+    ("slm_plan_sync", _c_int, [_vp]),
+    ("slm_plan_read", _c_int, [_vp, _vp, _vp, _vp, _vp]),
+    ("slm_plan_read_target_stats", _c_int, [_vp, _vp, _vp]),
+    ("slm_plan_kernel_bytes", ctypes.c_longlong, [_vp, _c_int]),
+    ("slm_plan_info", _c_int, [_vp, _vp]),
+    ("slm_gs", _c_int, [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_double, _vp, _vp, _vp, _vp, _vp]),
+    ("slm_gd", _c_int,
+     [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_double, _vp, _vp, _c_float, _vp, _vp, _vp, _vp]),
+    ("slm_fft2", _c_int, [_vp, _vp, _c_int, _c_int, _c_int, _c_int]),
+    ("slm_comm_unique_id", _c_int, [_vp]),
+    ("slm_comm_init", _c_int, [_c_int, _c_int, _vp]),
+    ("slm_comm_destroy", _c_int, []),
+    ("slm_plan_gather_phase", _c_int, [_vp, _vp, _c_int, _vp]),
+]
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libslm_hip.so once; raise ImportError if it was never built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(or `make -C spatial_light_modulator_module_amd/csrc`). There is no CPU fallback."
+        )
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, res, args in _SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def last_error() -> str:
+    msg = load().slm_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise SlmError(f"{what} failed ({rc}): {last_error()}")
+
+
+def ptr(a: np.ndarray | None) -> int | None:
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "arrays passed to libslm_hip must be C-contiguous"
+    return a.ctypes.data
+
+
+_initialised_device: int | None = None
+
+
+def init(device: int | None = None) -> None:
+    """Bind this process to one GPU (default: $SLM_DEVICE, $LOCAL_RANK or 0)."""
+    global _initialised_device
+    if device is None:
+        device = int(os.environ.get("SLM_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+    if _initialised_device == device:
+        return
+    check(load().slm_init(device), f"slm_init({device})")
+    _initialised_device = device
+
+
+def device_count() -> int:
+    return int(load().slm_device_count())
+
+
+class Plan:
+    """A device-resident batch of holograms (slm_plan_* in include/slm_hip.h)."""
+
+    def __init__(self, algo: int, batch: int, height: int, width: int, tgt_type: int, has_ain: bool,
+                 max_loops: int):
+        init()
+        self._lib = load()
+        h = ctypes.c_void_p()
+        check(self._lib.slm_plan_create(algo, batch, height, width, tgt_type, int(bool(has_ain)), max_loops,
+                                        ctypes.byref(h)), "slm_plan_create")
+        self.handle = h
+        self.algo, self.batch, self.height, self.width = algo, batch, height, width
+        self.tgt_type, self.has_ain, self.max_loops = tgt_type, bool(has_ain), max_loops
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            self._lib.slm_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def shape(self):
+        return (self.batch, self.height, self.width)
+
+    def set_target(self, tgt: np.ndarray) -> None:
+        dt = np.uint8 if self.tgt_type == TGT_U8 else np.float32
+        a = np.ascontiguousarray(tgt, dtype=dt).reshape(self.shape)
+        check(self._lib.slm_plan_set_target(self.handle, ptr(a)), "slm_plan_set_target")
+
+    def set_ain(self, ain: np.ndarray) -> None:
+        a = np.ascontiguousarray(ain, dtype=np.float32).reshape(self.height, self.width)
+        check(self._lib.slm_plan_set_ain(self.handle, ptr(a)), "slm_plan_set_ain")
+
+    def set_phase(self, phase: np.ndarray | None) -> None:
+        a = None if phase is None else np.ascontiguousarray(phase, dtype=np.float32).reshape(self.shape)
+        check(self._lib.slm_plan_set_phase(self.handle, ptr(a)), "slm_plan_set_phase")
+
+    def set_field(self, field: np.ndarray | None) -> None:
+        a = None
+        if field is not None:
+            a = np.ascontiguousarray(np.asarray(field).astype(np.complex64)).reshape(self.shape)
+            a = a.view(np.float32)
+        check(self._lib.slm_plan_set_field(self.handle, ptr(a)), "slm_plan_set_field")
+
+    def set_lr(self, lr: np.ndarray) -> None:
+        a = np.ascontiguousarray(lr, dtype=np.float32)
+        if a.size != self.max_loops:
+            raise ValueError(f"need {self.max_loops} learning rates, got {a.size}")
+        check(self._lib.slm_plan_set_lr(self.handle, ptr(a)), "slm_plan_set_lr")
+
+    def run(self, loops: int, tol: float = 0.0, checked: bool = False, white_attention: float = 0.0) -> None:
+        check(self._lib.slm_plan_run(self.handle, loops, float(tol), int(bool(checked)), float(white_attention)),
+              "slm_plan_run")
+
+    def run_timed(self, loops: int, tol: float = 0.0, checked: bool = False, white_attention: float = 0.0):
+        us = np.zeros(NUM_KERNEL_CLASSES, dtype=np.float64)
+        cnt = np.zeros(NUM_KERNEL_CLASSES, dtype=np.int32)
+        check(self._lib.slm_plan_run_timed(self.handle, loops, float(tol), int(bool(checked)),
+                                           float(white_attention), ptr(us), ptr(cnt)), "slm_plan_run_timed")
+        return us, cnt
+
+    def sync(self) -> None:
+        check(self._lib.slm_plan_sync(self.handle), "slm_plan_sync")
+
+    def read(self, phase=True, expected=True, stats=True, iters=True):
+        out_phase = np.empty(self.shape, np.float32) if phase else None
+        out_exp = np.empty(self.shape, np.float32) if expected else None
+        out_stats = np.empty((self.batch, self.max_loops, 4), np.float64) if stats else None
+        out_iters = np.empty(self.batch, np.int32) if iters else None
+        check(self._lib.slm_plan_read(self.handle, ptr(out_phase), ptr(out_exp), ptr(out_stats), ptr(out_iters)),
+              "slm_plan_read")
+        return out_phase, out_exp, out_stats, out_iters
+
+    def target_stats(self):
+        norm = np.empty(self.batch, np.float64)
+        st2 = np.empty(self.batch, np.float64)
+        check(self._lib.slm_plan_read_target_stats(self.handle, ptr(norm), ptr(st2)), "slm_plan_read_target_stats")
+        return norm, st2
+
+    def kernel_bytes(self, cls: int) -> int:
+        return int(self._lib.slm_plan_kernel_bytes(self.handle, cls))
+
+    def info(self) -> dict:
+        a = np.zeros(8, np.int32)
+        check(self._lib.slm_plan_info(self.handle, ptr(a)), "slm_plan_info")
+        return {"col_cw": int(a[0]), "col_workgroups": int(a[1]), "col_threads": int(a[2]),
+                "row_threads": int(a[3]), "rows_per_workgroup": int(a[4])}
+
+    def gather_phase(self, counts, root: int = 0, host_out: np.ndarray | None = None) -> None:
+        c = np.ascontiguousarray(counts, dtype=np.int32)
+        check(self._lib.slm_plan_gather_phase(self.handle, ptr(c), root, ptr(host_out)), "slm_plan_gather_phase")
+
+
+def fft2(x: np.ndarray, inverse: bool = False) -> np.ndarray:
+    """Unscaled 2-D C2C transform of [..., H, W] on the GPU (test entry)."""
+    init()
+    a = np.ascontiguousarray(x, dtype=np.complex64)
+    shape = a.shape
+    h, w = shape[-2:]
+    b = int(np.prod(shape[:-2])) if len(shape) > 2 else 1
+    out = np.empty_like(a)
+    check(load().slm_fft2(ptr(a.view(np.float32)), ptr(out.view(np.float32)), b, h, w, int(bool(inverse))),
+          "slm_fft2")
+    return out
+
+
+def comm_unique_id() -> bytes:
+    buf = (ctypes.c_ubyte * 128)()
+    check(load().slm_comm_unique_id(buf), "slm_comm_unique_id")
+    return bytes(buf)
+
+
+def comm_init(nranks: int, rank: int, uid: bytes) -> None:
+    init()
+    buf = (ctypes.c_ubyte * 128).from_buffer_copy(uid)
+    check(load().slm_comm_init(nranks, rank, buf), "slm_comm_init")
+
+
+def comm_destroy() -> None:
+    load().slm_comm_destroy()

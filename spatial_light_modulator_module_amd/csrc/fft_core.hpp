@@ -1,0 +1,293 @@
+// Device-side FFT engine for gfx950 (CDNA4): in-register small DFTs plus a
+// Stockham autosort driver whose passes exchange through LDS.
+//
+// Data model. A line of length N is spread over T = N / E threads; thread t
+// holds slot m = element (t + T * m). With that layout
+//   * the first pass reads its butterfly inputs straight from the slots, so a
+//     line can be loaded from HBM with lane-contiguous (coalesced) accesses;
+//   * the last pass leaves its outputs in the same slot layout in natural
+//     order, so results are stored coalesced and an element-wise projection can
+//     run in registers between an inverse and a forward transform with no LDS
+//     round trip (the fused GS/GD iteration relies on this).
+// Forward = exp(-2 pi i nk/N), unscaled (scipy.fft.fft2, src/algorithms.py:31);
+// inverse = exp(+2 pi i nk/N), unscaled (callers apply 1/N where needed).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <type_traits>
+#include <utility>
+
+#include "plans.hpp"
+
+namespace slm {
+
+// ------------------------------------------------------------------------
+// compile-time helpers
+// ------------------------------------------------------------------------
+template <int... Rs>
+struct IntList {};
+
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for_impl(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for_impl<I + 1, N>(f);
+    }
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    static_for_impl<0, N>(f);
+}
+
+template <int N, std::size_t... I>
+constexpr auto radices_of(std::index_sequence<I...>) {
+    return IntList<kPlans[plan_index(N)].r[I]...>{};
+}
+template <int N>
+using RadicesOf = decltype(radices_of<N>(std::make_index_sequence<kPlans[plan_index(N)].npass>{}));
+
+template <int N>
+struct PlanOf {
+    static_assert(plan_index(N) >= 0, "unsupported transform length");
+    static constexpr int E = kPlans[plan_index(N)].e;
+    static constexpr int T = N / E;
+    static constexpr int LINE = lds_line(N);
+};
+
+// cos(2 pi q / 48) for the constant twiddles of radix 2, 3, 4, 8, 12, 16.
+constexpr double kCos48[13] = {1.0,
+                               0.99144486137381041,
+                               0.96592582628906829,
+                               0.92387953251128674,
+                               0.86602540378443865,
+                               0.79335334029123517,
+                               0.70710678118654752,
+                               0.60876142900872063,
+                               0.5,
+                               0.38268343236508977,
+                               0.25881904510252076,
+                               0.13052619222005159,
+                               0.0};
+constexpr double cos48(int q) {
+    q = ((q % 48) + 48) % 48;
+    if (q <= 12) return kCos48[q];
+    if (q <= 24) return -kCos48[24 - q];
+    if (q <= 36) return -kCos48[q - 24];
+    return kCos48[48 - q];
+}
+constexpr double sin48(int q) { return cos48(q - 12); }
+
+// ------------------------------------------------------------------------
+// complex helpers (float2 = interleaved complex64, the HBM layout)
+// ------------------------------------------------------------------------
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+// a * conj(b)
+__device__ __forceinline__ float2 cmulc(float2 a, float2 b) {
+    return make_float2(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
+}
+
+// Multiply by the constant twiddle w_R^K (forward: exp(-2 pi i K/R)).
+template <int K, int R, bool INV>
+__device__ __forceinline__ float2 twc(float2 a) {
+    constexpr int q = ((48 / R) * K) % 48;
+    if constexpr (q == 0) {
+        return a;
+    } else if constexpr (q == 24) {
+        return make_float2(-a.x, -a.y);
+    } else if constexpr (q == 12) {  // forward: * (-i)
+        return INV ? make_float2(-a.y, a.x) : make_float2(a.y, -a.x);
+    } else if constexpr (q == 36) {  // forward: * (+i)
+        return INV ? make_float2(a.y, -a.x) : make_float2(-a.y, a.x);
+    } else {
+        constexpr float c = (float)cos48(q);
+        constexpr float s = (float)(INV ? sin48(q) : -sin48(q));
+        return make_float2(a.x * c - a.y * s, a.x * s + a.y * c);
+    }
+}
+
+// ------------------------------------------------------------------------
+// in-register DFTs, natural order in and out
+// ------------------------------------------------------------------------
+template <int R, bool INV>
+struct Dft;
+
+template <bool INV>
+struct Dft<1, INV> {
+    __device__ __forceinline__ static void run(float2*) {}
+};
+
+template <bool INV>
+struct Dft<2, INV> {
+    __device__ __forceinline__ static void run(float2* v) {
+        const float2 a = v[0], b = v[1];
+        v[0] = cadd(a, b);
+        v[1] = csub(a, b);
+    }
+};
+
+template <bool INV>
+struct Dft<3, INV> {
+    __device__ __forceinline__ static void run(float2* v) {
+        constexpr float h = 0.86602540378443865f;  // sqrt(3)/2
+        const float2 s = cadd(v[1], v[2]);
+        const float2 d = csub(v[1], v[2]);
+        const float2 t = make_float2(v[0].x - 0.5f * s.x, v[0].y - 0.5f * s.y);
+        // forward: (-i) * h * d ; inverse: (+i) * h * d
+        const float2 m = INV ? make_float2(-h * d.y, h * d.x) : make_float2(h * d.y, -h * d.x);
+        v[0] = cadd(v[0], s);
+        v[1] = cadd(t, m);
+        v[2] = csub(t, m);
+    }
+};
+
+template <bool INV>
+struct Dft<4, INV> {
+    __device__ __forceinline__ static void run(float2* v) {
+        const float2 a = cadd(v[0], v[2]);
+        const float2 b = csub(v[0], v[2]);
+        const float2 c = cadd(v[1], v[3]);
+        const float2 d = twc<1, 4, INV>(csub(v[1], v[3]));
+        v[0] = cadd(a, c);
+        v[2] = csub(a, c);
+        v[1] = cadd(b, d);
+        v[3] = csub(b, d);
+    }
+};
+
+// Cooley-Tukey split R = R1 * R2: n = R2 n1 + n2, k = k1 + R1 k2.
+template <int R1, int R2, bool INV>
+__device__ __forceinline__ void dft_split(float2* v) {
+    constexpr int R = R1 * R2;
+    float2 z[R];
+    static_for<R2>([&](auto n2c) {
+        constexpr int n2 = decltype(n2c)::value;
+        float2 col[R1];
+        static_for<R1>([&](auto n1c) {
+            constexpr int n1 = decltype(n1c)::value;
+            col[n1] = v[R2 * n1 + n2];
+        });
+        Dft<R1, INV>::run(col);
+        static_for<R1>([&](auto k1c) {
+            constexpr int k1 = decltype(k1c)::value;
+            z[n2 * R1 + k1] = twc<n2 * k1, R, INV>(col[k1]);
+        });
+    });
+    static_for<R1>([&](auto k1c) {
+        constexpr int k1 = decltype(k1c)::value;
+        float2 row[R2];
+        static_for<R2>([&](auto n2c) {
+            constexpr int n2 = decltype(n2c)::value;
+            row[n2] = z[n2 * R1 + k1];
+        });
+        Dft<R2, INV>::run(row);
+        static_for<R2>([&](auto k2c) {
+            constexpr int k2 = decltype(k2c)::value;
+            v[k1 + R1 * k2] = row[k2];
+        });
+    });
+}
+
+template <bool INV>
+struct Dft<8, INV> {
+    __device__ __forceinline__ static void run(float2* v) { dft_split<2, 4, INV>(v); }
+};
+template <bool INV>
+struct Dft<12, INV> {
+    __device__ __forceinline__ static void run(float2* v) { dft_split<4, 3, INV>(v); }
+};
+template <bool INV>
+struct Dft<16, INV> {
+    __device__ __forceinline__ static void run(float2* v) { dft_split<4, 4, INV>(v); }
+};
+
+// ------------------------------------------------------------------------
+// LDS views. A pass writes output element o and reads element t + T m of the
+// line; padding one slot per 16 keeps the strided first-pass writes off a
+// single bank.
+// ------------------------------------------------------------------------
+struct LdsLine {  // one transform line per thread group (row kernels)
+    float2* base;
+    __device__ __forceinline__ void store(int o, float2 v) const { base[o + (o >> 4)] = v; }
+    __device__ __forceinline__ float2 load(int o) const { return base[o + (o >> 4)]; }
+};
+
+template <int CW>
+struct LdsTile {  // CW interleaved columns (column kernels): [o][c]
+    float2* base;
+    int c;
+    __device__ __forceinline__ void store(int o, float2 v) const { base[(o + (o >> 4)) * CW + c] = v; }
+    __device__ __forceinline__ float2 load(int o) const { return base[(o + (o >> 4)) * CW + c]; }
+};
+
+// ------------------------------------------------------------------------
+// Stockham driver. v[m] holds element t + T m on entry (any order of the
+// line's data in the slot layout) and the transform's element t + T m on exit.
+// Twiddles of the passes after the first come from the per-length table
+// `tw` (forward convention; conjugated here for the inverse).
+// ------------------------------------------------------------------------
+template <int N, int E, bool INV, int Ns, int TwOff, class Lds, int R, int... Rest>
+__device__ __forceinline__ void stockham_pass(float2 (&v)[E], int t, const float2* __restrict__ tw, const Lds& lds) {
+    constexpr int T = N / E;
+    constexpr int NB = E / R;
+    static_assert(E % R == 0, "radix must divide elements per thread");
+    static_for<NB>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        const int b = t + k * T;
+        const int j = (Ns == 1) ? 0 : (b % Ns);
+        float2 u[R];
+        static_for<R>([&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            u[r] = v[k + r * NB];
+        });
+        if constexpr (Ns > 1) {
+            static_for<R - 1>([&](auto rc) {
+                constexpr int r = decltype(rc)::value + 1;
+                const float2 w = tw[TwOff + (r - 1) * Ns + j];
+                u[r] = INV ? cmulc(u[r], w) : cmul(u[r], w);
+            });
+        }
+        Dft<R, INV>::run(u);
+        if constexpr (sizeof...(Rest) == 0) {
+            // last pass: Ns * R == N, so b < Ns and output r lands in slot k + r NB
+            static_for<R>([&](auto rc) {
+                constexpr int r = decltype(rc)::value;
+                v[k + r * NB] = u[r];
+            });
+        } else {
+            const int o = (b / Ns) * Ns * R + j;
+            static_for<R>([&](auto rc) {
+                constexpr int r = decltype(rc)::value;
+                lds.store(o + r * Ns, u[r]);
+            });
+        }
+    });
+    if constexpr (sizeof...(Rest) > 0) {
+        __syncthreads();
+        static_for<E>([&](auto mc) {
+            constexpr int m = decltype(mc)::value;
+            v[m] = lds.load(t + m * T);
+        });
+        __syncthreads();
+        constexpr int kNextOff = TwOff + (Ns > 1 ? (R - 1) * Ns : 0);
+        stockham_pass<N, E, INV, Ns * R, kNextOff, Lds, Rest...>(v, t, tw, lds);
+    }
+}
+
+template <int N, bool INV, class Lds, int... Rs>
+__device__ __forceinline__ void fft_line_impl(float2 (&v)[PlanOf<N>::E], int t, const float2* __restrict__ tw,
+                                              const Lds& lds, IntList<Rs...>) {
+    stockham_pass<N, PlanOf<N>::E, INV, 1, 0, Lds, Rs...>(v, t, tw, lds);
+}
+
+// Transform one line held in the slot layout. Every thread of the workgroup
+// must call this (it contains workgroup barriers).
+template <int N, bool INV, class Lds>
+__device__ __forceinline__ void fft_line(float2 (&v)[PlanOf<N>::E], int t, const float2* __restrict__ tw,
+                                         const Lds& lds) {
+    fft_line_impl<N, INV>(v, t, tw, lds, RadicesOf<N>{});
+}
+
+}  // namespace slm

@@ -1,0 +1,464 @@
+// Fused GS / GD iteration kernels for gfx950.
+//
+// One GS iteration of the reference (src/algorithms.py:30-38)
+//     B = a_in exp(i angle A); C = fft2(B); D = |a_T| exp(i angle C); A = ifft2(D)
+// is split at the separable 2-D transform boundaries so that every HBM round
+// trip does useful work on both sides of it:
+//     col pass : X --fwd col FFT--> C --stats, D = a_T C/|C|--> --inv col FFT--> Y
+//     row pass : Y --inv row FFT--> A --B = a_in A/|A|-->      --fwd row FFT--> X
+// X holds the row-transformed B, Y the column-inverse-transformed D. The 1/S of
+// ifft2 is dropped (the projections are scale free; only angles leave the
+// loop). Per pixel and iteration this moves 8+8 B per pass plus the target:
+// 36 B (f32 target) or 33 B (u8 target) instead of 68 B for unfused 2-D FFTs.
+//
+// GD (src/algorithms.py:83-93) needs the global max of |F|^2 before the
+// gradient can be formed, so its column side is two launches (stats, then
+// recompute F and build the gradient) and its row side fuses the inverse row
+// transform, the x/|x| Jacobian-transpose, the update and the next forward row
+// transform.
+#pragma once
+#include <hip/hip_fp16.h>
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fft_core.hpp"
+
+namespace slm {
+
+// ------------------------------------------------------------------------
+// launch parameter blocks (one struct per kernel family => uniform signatures)
+// ------------------------------------------------------------------------
+struct RowParams {
+    const float2* in;        // row-pass input (Y, or X for the debug FFT)
+    float2* out;             // row-pass output (X)
+    const float* ain;        // incoming amplitude [H][W], nullptr = uniform 1
+    const float* phase_in;   // warm-start phase [B][H][W]
+    float* phase_out;        // output phase [B][H][W]
+    float2* field;           // GD state x [B][H][W]
+    const float* lr;         // GD learning rate per iteration
+    const int* stop_iter;    // [B], INT_MAX while running
+    int iter;                // iteration index of this launch
+    int W;                   // row length (== template W; kept for checks)
+    long long holo;          // elements per hologram (H * W)
+    float inv_s;             // 1 / (H * W)
+    const float2* tw;        // twiddle table for length W
+};
+
+struct ColParams {
+    const float2* in;        // column-pass input X
+    const float2* in_alt;    // GD ping-pong partner (expected-output kernel)
+    float2* out;             // column-pass output Y
+    const void* tgt;         // target intensity T [B][H][W] (uint8 or float)
+    double* partials;        // [B][max_loops][nwg] x 4 doubles: max, sum E^2, sum E T, 0
+    float* e_out;            // |C|^2 of the final iteration [B][H][W]
+    const int* stop_iter;    // [B]
+    const float* norm;       // max(T) per hologram
+    int iter;                // iteration index of this launch
+    int max_loops;           // partial-slab stride
+    int loops;               // iterations of this run
+    int W;                   // image width (row stride)
+    int nwg;                 // column workgroups per hologram (W / CW)
+    long long holo;          // elements per hologram
+    float wa;                // GD white_attention
+    const float2* tw;        // twiddle table for length H
+};
+
+enum RowMode : int {
+    ROW_GS_MAIN = 0,      // Y -> inv -> a_in A/|A| -> fwd -> X
+    ROW_GS_PHASE = 1,     // Y -> inv -> angle -> phase_out
+    ROW_PHASE_FWD = 2,    // phase_in -> a_in e^{i phi} -> fwd -> X (warm start)
+    ROW_GD_INIT_Y = 3,    // Y -> inv -> x = a_in A/|A| (fourier guess) -> field, fwd(x/|x| a_in) -> X
+    ROW_GD_INIT_FIELD = 4,// field -> fwd(x/|x| a_in) -> X
+    ROW_GD_MAIN = 5,      // Y -> inv -> gradient, update field -> fwd -> X
+    ROW_FFT_FWD = 6,      // in -> fwd -> out (test entry)
+    ROW_FFT_INV = 7,      // in -> inv -> out (test entry)
+    ROW_NUM_MODES = 8
+};
+
+enum ColMode : int {
+    COL_GS_MAIN = 0,      // X -> fwd -> stats, a_T C/|C| -> inv -> Y
+    COL_REAL_INV = 1,     // T -> a_T -> inv -> Y (cold start, fourier guess)
+    COL_EXPECTED = 2,     // X -> fwd -> |C|^2 -> e_out
+    COL_GD_STATS = 3,     // X -> fwd -> stats of P = |F|^2
+    COL_GD_GRAD = 4,      // X -> fwd -> mask F (sP - T) -> inv -> Y
+    COL_FFT_FWD = 5,      // in -> fwd -> out (test entry)
+    COL_FFT_INV = 6,      // in -> inv -> out (test entry)
+    COL_NUM_MODES = 7
+};
+
+// target element types: 0 = uint8 (amplitude rounded to float16 as numpy's
+// sqrt(uint8) does), 1 = float32 (amplitude = sqrtf).
+enum TgtType : int { TGT_U8 = 0, TGT_F32 = 1, TGT_NUM = 2 };
+
+using RowFn = void (*)(RowParams);
+using ColFn = void (*)(ColParams);
+
+// ------------------------------------------------------------------------
+// geometry
+// ------------------------------------------------------------------------
+template <int W>
+struct RowCfg {
+    static constexpr int T = PlanOf<W>::T;
+    static constexpr int RPW = (T >= 256) ? 1 : 256 / T;  // rows per workgroup
+    static constexpr int THREADS = RPW * T;
+};
+
+template <int H, int CW>
+struct ColCfg {
+    static constexpr int T = PlanOf<H>::T;
+    static constexpr int THREADS = CW * T;
+    static constexpr bool kValid = THREADS >= 64 && THREADS <= 1024 && lds_line(H) * CW * 8 <= 160 * 1024;
+};
+
+// XCD-aware bijective remap: blocks that share (id % 8) — one XCD under the
+// observed round-robin dispatch — get consecutive logical column groups, so
+// the partial 128-B lines of narrow column tiles are shared through one L2.
+// Speed only; correctness does not depend on placement.
+__device__ __forceinline__ int xcd_remap(int id, int n) {
+    const int q = n >> 3, r = n & 7;
+    const int xcd = id & 7, k = id >> 3;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+}
+
+// ------------------------------------------------------------------------
+// element-wise pieces
+// ------------------------------------------------------------------------
+// a * z / |z|, with angle(0) = 0 -> a (np.angle(0) == 0, src/algorithms.py:30,33).
+__device__ __forceinline__ float2 unit_scale(float2 z, float a) {
+    const float n2 = z.x * z.x + z.y * z.y;
+    if (n2 == 0.0f) return make_float2(a, 0.0f);
+    const float r = a * rsqrtf(n2);
+    return make_float2(z.x * r, z.y * r);
+}
+
+template <int TT>
+struct TgtLoad;
+template <>
+struct TgtLoad<TGT_U8> {
+    __device__ __forceinline__ static float load(const void* p, long long i) {
+        return (float)static_cast<const uint8_t*>(p)[i];
+    }
+    __device__ __forceinline__ static float amp(float t) { return __half2float(__float2half_rn(sqrtf(t))); }
+};
+template <>
+struct TgtLoad<TGT_F32> {
+    __device__ __forceinline__ static float load(const void* p, long long i) {
+        return static_cast<const float*>(p)[i];
+    }
+    __device__ __forceinline__ static float amp(float t) { return sqrtf(t); }
+};
+
+// Block-wide reduction of (max, sum, sum); result valid in thread 0.
+template <int THREADS>
+__device__ __forceinline__ void block_reduce_stats(double& mx, double& s2, double& st) {
+    constexpr int NW = (THREADS + 63) / 64;
+    __shared__ double red[NW][3];
+    for (int off = 32; off > 0; off >>= 1) {
+        mx = fmax(mx, __shfl_xor(mx, off));
+        s2 += __shfl_xor(s2, off);
+        st += __shfl_xor(st, off);
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (NW > 1) {
+        if (lane == 0) {
+            red[wid][0] = mx;
+            red[wid][1] = s2;
+            red[wid][2] = st;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int w = 1; w < NW; ++w) {
+                mx = fmax(mx, red[w][0]);
+                s2 += red[w][1];
+                st += red[w][2];
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------
+// row pass
+// ------------------------------------------------------------------------
+template <int W, int MODE>
+__global__ void __launch_bounds__(RowCfg<W>::THREADS) row_kernel(RowParams p) {
+    constexpr int E = PlanOf<W>::E;
+    constexpr int T = PlanOf<W>::T;
+    constexpr int RPW = RowCfg<W>::RPW;
+    constexpr int LINE = PlanOf<W>::LINE;
+    __shared__ float2 smem[RPW * LINE];
+
+    const int b = blockIdx.y;
+    if constexpr (MODE == ROW_GS_MAIN) {
+        if (p.iter >= p.stop_iter[b]) return;  // stopped after this iteration's column pass
+    } else if constexpr (MODE == ROW_GD_MAIN) {
+        if (p.iter > p.stop_iter[b]) return;
+    }
+    const int q = threadIdx.x / T;
+    const int t = threadIdx.x - q * T;
+    const int row = blockIdx.x * RPW + q;
+    const long long roff = (long long)row * W;
+    const long long off = (long long)b * p.holo + roff;
+    const LdsLine lds{smem + q * LINE};
+    float2 v[E];
+
+    auto ain_at = [&](int m) -> float { return p.ain ? p.ain[roff + t + T * m] : 1.0f; };
+
+    if constexpr (MODE == ROW_PHASE_FWD) {
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            float s, c;
+            sincosf(p.phase_in[off + t + T * m], &s, &c);
+            const float a = ain_at(m);
+            v[m] = make_float2(a * c, a * s);
+        }
+    } else if constexpr (MODE == ROW_GD_INIT_FIELD) {
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const float2 x = p.field[off + t + T * m];
+            const float a = ain_at(m);
+            const float r = rsqrtf(x.x * x.x + x.y * x.y);
+            v[m] = make_float2(x.x * r * a, x.y * r * a);
+        }
+    } else {
+#pragma unroll
+        for (int m = 0; m < E; ++m) v[m] = p.in[off + t + T * m];
+    }
+
+    if constexpr (MODE == ROW_GS_MAIN || MODE == ROW_GS_PHASE || MODE == ROW_GD_INIT_Y || MODE == ROW_GD_MAIN ||
+                  MODE == ROW_FFT_INV) {
+        fft_line<W, true>(v, t, p.tw, lds);
+    }
+
+    if constexpr (MODE == ROW_GS_PHASE) {
+#pragma unroll
+        for (int m = 0; m < E; ++m) p.phase_out[off + t + T * m] = atan2f(v[m].y, v[m].x);
+        return;
+    } else if constexpr (MODE == ROW_FFT_INV) {
+#pragma unroll
+        for (int m = 0; m < E; ++m) p.out[off + t + T * m] = v[m];
+        return;
+    } else {
+        if constexpr (MODE == ROW_GS_MAIN) {
+#pragma unroll
+            for (int m = 0; m < E; ++m) v[m] = unit_scale(v[m], ain_at(m));
+        } else if constexpr (MODE == ROW_GD_INIT_Y) {
+#pragma unroll
+            for (int m = 0; m < E; ++m) {
+                const float a = ain_at(m);
+                const float2 x = unit_scale(v[m], a);  // a_in exp(i angle(ifft2(sqrt T)))
+                p.field[off + t + T * m] = x;
+                const float r = rsqrtf(x.x * x.x + x.y * x.y);
+                v[m] = make_float2(x.x * r * a, x.y * r * a);
+            }
+        } else if constexpr (MODE == ROW_GD_MAIN) {
+            // dEdF = ifft2(...) * a_in (src/algorithms.py:87-89); dEdX_complex (:179-185);
+            // input -= lr * dEdX (:91); next forward input x/|x| a_in (:84).
+            const float lr = p.lr[p.iter];
+#pragma unroll
+            for (int m = 0; m < E; ++m) {
+                const float a = ain_at(m);
+                const float2 g = make_float2(v[m].x * p.inv_s * a, v[m].y * p.inv_s * a);
+                const long long idx = off + t + T * m;
+                float2 x = p.field[idx];
+                const float ax2 = x.x * x.x + x.y * x.y;
+                const float inv = 1.0f / sqrtf(ax2);
+                const float inv3 = inv * inv * inv;
+                const float re = x.x * g.x + x.y * g.y;
+                const float dx = g.x * inv - x.x * re * inv3;
+                const float dy = g.y * inv - x.y * re * inv3;
+                x.x -= lr * dx;
+                x.y -= lr * dy;
+                p.field[idx] = x;
+                const float r = rsqrtf(x.x * x.x + x.y * x.y);
+                v[m] = make_float2(x.x * r * a, x.y * r * a);
+            }
+        }
+        fft_line<W, false>(v, t, p.tw, lds);
+#pragma unroll
+        for (int m = 0; m < E; ++m) p.out[off + t + T * m] = v[m];
+    }
+}
+
+// ------------------------------------------------------------------------
+// column pass
+// ------------------------------------------------------------------------
+template <int H, int CW, int MODE, int TT>
+__global__ void __launch_bounds__((ColCfg<H, CW>::THREADS)) col_kernel(ColParams p) {
+    constexpr int E = PlanOf<H>::E;
+    constexpr int T = PlanOf<H>::T;
+    constexpr int LINE = PlanOf<H>::LINE;
+    constexpr int THREADS = ColCfg<H, CW>::THREADS;
+    __shared__ float2 smem[LINE * CW];
+
+    const int b = blockIdx.y;
+    if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_STATS || MODE == COL_GD_GRAD) {
+        if (p.iter > p.stop_iter[b]) return;
+    }
+    const int wg = xcd_remap(blockIdx.x, gridDim.x);
+    const int c = threadIdx.x % CW;
+    const int t = threadIdx.x / CW;
+    const int x = wg * CW + c;
+    const long long base = (long long)b * p.holo + x;
+    const LdsTile<CW> lds{smem, c};
+    float2 v[E];
+
+    // GD gradient needs this iteration's global max of |F|^2 (src/algorithms.py:86).
+    float maxp = 0.0f;
+    if constexpr (MODE == COL_GD_GRAD) {
+        __shared__ float smax;
+        const double* part = p.partials + ((long long)b * p.max_loops + p.iter) * p.nwg * 4;
+        double m = 0.0;
+        for (int k = threadIdx.x; k < p.nwg; k += THREADS) m = fmax(m, part[k * 4]);
+        double d1 = 0.0, d2 = 0.0;
+        block_reduce_stats<THREADS>(m, d1, d2);
+        if (threadIdx.x == 0) smax = (float)m;
+        __syncthreads();
+        maxp = smax;
+    }
+
+    if constexpr (MODE == COL_REAL_INV) {
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const float tv = TgtLoad<TT>::load(p.tgt, base + (long long)(t + T * m) * p.W);
+            v[m] = make_float2(TgtLoad<TT>::amp(tv), 0.0f);
+        }
+    } else if constexpr (MODE == COL_EXPECTED) {
+        // GD keeps X of iteration i in buffer i % 2; GS passes the same buffer twice.
+        const int s = min(p.stop_iter[b], p.loops - 1);
+        const float2* src = (s & 1) ? p.in_alt : p.in;
+#pragma unroll
+        for (int m = 0; m < E; ++m) v[m] = src[base + (long long)(t + T * m) * p.W];
+    } else {
+#pragma unroll
+        for (int m = 0; m < E; ++m) v[m] = p.in[base + (long long)(t + T * m) * p.W];
+    }
+
+    if constexpr (MODE == COL_REAL_INV || MODE == COL_FFT_INV) {
+        fft_line<H, true>(v, t, p.tw, lds);
+#pragma unroll
+        for (int m = 0; m < E; ++m) p.out[base + (long long)(t + T * m) * p.W] = v[m];
+        return;
+    } else {
+        fft_line<H, false>(v, t, p.tw, lds);
+    }
+
+    if constexpr (MODE == COL_FFT_FWD) {
+#pragma unroll
+        for (int m = 0; m < E; ++m) p.out[base + (long long)(t + T * m) * p.W] = v[m];
+        return;
+    } else if constexpr (MODE == COL_EXPECTED) {
+#pragma unroll
+        for (int m = 0; m < E; ++m)
+            p.e_out[base + (long long)(t + T * m) * p.W] = v[m].x * v[m].x + v[m].y * v[m].y;
+        return;
+    } else {
+        double mx = 0.0, s2 = 0.0, st = 0.0;
+        const float norm = (MODE == COL_GD_GRAD) ? p.norm[b] : 0.0f;
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const float tv = TgtLoad<TT>::load(p.tgt, base + (long long)(t + T * m) * p.W);
+            const float e = v[m].x * v[m].x + v[m].y * v[m].y;
+            if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_STATS) {
+                const double ed = (double)e;
+                mx = fmax(mx, ed);
+                s2 += ed * ed;
+                st += ed * (double)tv;
+            }
+            if constexpr (MODE == COL_GS_MAIN) {
+                v[m] = unit_scale(v[m], TgtLoad<TT>::amp(tv));
+            } else if constexpr (MODE == COL_GD_GRAD) {
+                // mask * F * (output - T), output = |F|^2 norm / max (src/algorithms.py:80,85-88)
+                const float o = e * norm / maxp;
+                const float w = (1.0f + p.wa * tv / 255.0f) * (o - tv);
+                v[m] = make_float2(v[m].x * w, v[m].y * w);
+            }
+        }
+        if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_STATS) {
+            block_reduce_stats<THREADS>(mx, s2, st);
+            if (threadIdx.x == 0) {
+                double* dst = p.partials + (((long long)b * p.max_loops + p.iter) * p.nwg + wg) * 4;
+                dst[0] = mx;
+                dst[1] = s2;
+                dst[2] = st;
+                dst[3] = 0.0;
+            }
+        }
+        if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD) {
+            fft_line<H, true>(v, t, p.tw, lds);
+#pragma unroll
+            for (int m = 0; m < E; ++m) p.out[base + (long long)(t + T * m) * p.W] = v[m];
+        }
+    }
+}
+
+// ------------------------------------------------------------------------
+// small kernels (size independent)
+// ------------------------------------------------------------------------
+struct StatsParams {
+    const double* partials;  // [B][max_loops][nwg][4]
+    double* stats;           // [B][max_loops][4]: max, sum E^2, sum E T, err
+    int* stop_iter;          // [B]
+    const double* norm;      // [B] max(T)
+    const double* sum_t2;    // [B] sum T^2
+    double inv_s;            // 1 / S
+    double tol;
+    int max_loops;
+    int nwg;
+    int iter;                // finalize: iteration to check; reduce: unused
+};
+
+// Deterministic reduction of one (hologram, iteration) slab; 256 threads.
+__device__ __forceinline__ void reduce_slab(const StatsParams& p, int b, int i, double* out4) {
+    const double* part = p.partials + ((long long)b * p.max_loops + i) * p.nwg * 4;
+    double mx = 0.0, s2 = 0.0, st = 0.0;
+    for (int k = threadIdx.x; k < p.nwg; k += 256) {
+        mx = fmax(mx, part[k * 4 + 0]);
+        s2 += part[k * 4 + 1];
+        st += part[k * 4 + 2];
+    }
+    block_reduce_stats<256>(mx, s2, st);
+    if (threadIdx.x == 0) {
+        // error_f (src/algorithms.py:161-162) of E * norm / max(E) against T,
+        // expanded so that E never has to be stored: (s^2 SE2 - 2 s SET + ST2) / S.
+        const double s = __ddiv_rn(p.norm[b], mx);
+        double a = __dmul_rn(__dmul_rn(s, s), s2);
+        double c = __dmul_rn(__dmul_rn(2.0, s), st);
+        const double err = __dmul_rn(__dadd_rn(__dsub_rn(a, c), p.sum_t2[b]), p.inv_s);
+        out4[0] = mx;
+        out4[1] = s2;
+        out4[2] = st;
+        out4[3] = err;
+    }
+}
+
+#ifdef SLM_DEFINE_SMALL_KERNELS  // defined by exactly one translation unit (slm_capi.hip)
+__global__ void __launch_bounds__(256) stats_reduce_kernel(StatsParams p) {
+    const int i = blockIdx.x, b = blockIdx.y;
+    const int last = min(p.stop_iter[b], p.max_loops - 1);
+    if (i > last) return;
+    __shared__ double o[4];
+    reduce_slab(p, b, i, o);
+    if (threadIdx.x == 0)
+        for (int k = 0; k < 4; ++k) p.stats[((long long)b * p.max_loops + i) * 4 + k] = o[k];
+}
+
+// Tolerance check of one iteration (while error > tolerance, src/algorithms.py:29,83).
+__global__ void __launch_bounds__(256) stats_finalize_kernel(StatsParams p) {
+    const int b = blockIdx.x;
+    if (p.iter > p.stop_iter[b]) return;
+    __shared__ double o[4];
+    reduce_slab(p, b, p.iter, o);
+    if (threadIdx.x == 0) {
+        if (!(o[3] > p.tol)) p.stop_iter[b] = p.iter;
+    }
+}
+
+// hologram = np.angle(input) of the GD field (src/algorithms.py:111).
+__global__ void __launch_bounds__(256) field_phase_kernel(const float2* field, float* phase, long long n) {
+    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+        phase[i] = atan2f(field[i].y, field[i].x);
+}
+
+#endif  // SLM_DEFINE_SMALL_KERNELS
+
+}  // namespace slm

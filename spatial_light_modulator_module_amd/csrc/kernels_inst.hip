@@ -1,0 +1,72 @@
+// Instantiates every row / column kernel for one transform length SLM_N.
+// Compiled once per supported length (see Makefile) so the builds run in
+// parallel; dispatch.hip maps (length, mode, ...) to these tables.
+#include "dispatch.hpp"
+#include "kernels.hpp"
+
+#ifndef SLM_N
+#error "compile with -DSLM_N=<length>"
+#endif
+
+#define SLM_PASTE2(a, b) a##b
+#define SLM_PASTE(a, b) SLM_PASTE2(a, b)
+
+namespace slm {
+namespace {
+
+template <int N>
+RowFn row_table(int mode) {
+    switch (mode) {
+        case ROW_GS_MAIN: return row_kernel<N, ROW_GS_MAIN>;
+        case ROW_GS_PHASE: return row_kernel<N, ROW_GS_PHASE>;
+        case ROW_PHASE_FWD: return row_kernel<N, ROW_PHASE_FWD>;
+        case ROW_GD_INIT_Y: return row_kernel<N, ROW_GD_INIT_Y>;
+        case ROW_GD_INIT_FIELD: return row_kernel<N, ROW_GD_INIT_FIELD>;
+        case ROW_GD_MAIN: return row_kernel<N, ROW_GD_MAIN>;
+        case ROW_FFT_FWD: return row_kernel<N, ROW_FFT_FWD>;
+        case ROW_FFT_INV: return row_kernel<N, ROW_FFT_INV>;
+        default: return nullptr;
+    }
+}
+
+template <int N, int CW>
+ColFn col_table_cw(int mode, int tt) {
+    if constexpr (!ColCfg<N, CW>::kValid) {
+        return nullptr;
+    } else {
+        const bool u8 = (tt == TGT_U8);
+        switch (mode) {
+            case COL_GS_MAIN:
+                return u8 ? col_kernel<N, CW, COL_GS_MAIN, TGT_U8> : col_kernel<N, CW, COL_GS_MAIN, TGT_F32>;
+            case COL_REAL_INV:
+                return u8 ? col_kernel<N, CW, COL_REAL_INV, TGT_U8> : col_kernel<N, CW, COL_REAL_INV, TGT_F32>;
+            case COL_GD_STATS:
+                return u8 ? col_kernel<N, CW, COL_GD_STATS, TGT_U8> : col_kernel<N, CW, COL_GD_STATS, TGT_F32>;
+            case COL_GD_GRAD:
+                return u8 ? col_kernel<N, CW, COL_GD_GRAD, TGT_U8> : col_kernel<N, CW, COL_GD_GRAD, TGT_F32>;
+            case COL_EXPECTED: return col_kernel<N, CW, COL_EXPECTED, TGT_F32>;
+            case COL_FFT_FWD: return col_kernel<N, CW, COL_FFT_FWD, TGT_F32>;
+            case COL_FFT_INV: return col_kernel<N, CW, COL_FFT_INV, TGT_F32>;
+            default: return nullptr;
+        }
+    }
+}
+
+}  // namespace
+
+RowFn SLM_PASTE(row_fn_, SLM_N)(int mode) { return row_table<SLM_N>(mode); }
+
+ColFn SLM_PASTE(col_fn_, SLM_N)(int cw, int mode, int tt) {
+    switch (cw) {
+        case 4: return col_table_cw<SLM_N, 4>(mode, tt);
+        case 8: return col_table_cw<SLM_N, 8>(mode, tt);
+        case 16: return col_table_cw<SLM_N, 16>(mode, tt);
+        default: return nullptr;
+    }
+}
+
+int SLM_PASTE(row_threads_, SLM_N)() { return RowCfg<SLM_N>::THREADS; }
+int SLM_PASTE(row_rpw_, SLM_N)() { return RowCfg<SLM_N>::RPW; }
+int SLM_PASTE(col_threads_, SLM_N)(int cw) { return cw * PlanOf<SLM_N>::T; }
+
+}  // namespace slm

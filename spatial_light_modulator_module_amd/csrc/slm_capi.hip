@@ -1,0 +1,802 @@
+// libslm_hip.so host runtime: plans (device-resident batches), launch
+// sequencing of the fused GS / GD iterations, HIP-event timing, and the
+// RCCL gather of phases for one-process-per-GPU runs. C-ABI in
+// include/slm_hip.h.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/slm_hip.h"
+#include "dispatch.hpp"
+#define SLM_DEFINE_SMALL_KERNELS
+#include "kernels.hpp"
+
+using namespace slm;
+
+namespace {
+
+thread_local std::string g_err;
+int g_device = -1;
+std::mutex g_mu;
+std::map<std::pair<int, int>, float2*> g_twiddles;  // (device, n) -> table
+ncclComm_t g_comm = nullptr;
+int g_comm_rank = 0, g_comm_size = 1;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                              \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess)                                                                      \
+            return fail(SLM_ERR_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+                        __LINE__);                                                                 \
+    } while (0)
+
+#define NCCL_TRY(expr)                                                                                       \
+    do {                                                                                                     \
+        ncclResult_t r_ = (expr);                                                                            \
+        if (r_ != ncclSuccess) return fail(SLM_ERR_COMM, "%s failed: %s", #expr, ncclGetErrorString(r_)); \
+    } while (0)
+
+int ensure_device() {
+    if (g_device >= 0) {
+        HIP_TRY(hipSetDevice(g_device));
+        return 0;
+    }
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= 0)
+        return fail(SLM_ERR_HIP, "no HIP device available (%s); libslm_hip has no CPU path",
+                    hipGetErrorString(e));
+    g_device = 0;
+    HIP_TRY(hipSetDevice(0));
+    return 0;
+}
+
+// Twiddle table of one transform length, in the pass order of kPlans:
+// entry [(r - 1) * Ns + j] = exp(-2 pi i j r / (Ns R)), computed in double.
+int get_twiddles(int n, const float2** out) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto key = std::make_pair(g_device, n);
+    auto it = g_twiddles.find(key);
+    if (it != g_twiddles.end()) {
+        *out = it->second;
+        return 0;
+    }
+    const int pi = plan_index(n);
+    if (pi < 0) return fail(SLM_ERR_UNSUPPORTED, "unsupported transform length %d", n);
+    const RadixPlan& pl = kPlans[pi];
+    std::vector<float2> host;
+    host.reserve(twiddle_count(n) + 1);
+    int ns = 1;
+    for (int k = 0; k < pl.npass; ++k) {
+        const int r_ = pl.r[k];
+        if (ns > 1) {
+            const long long L = (long long)ns * r_;
+            for (int r = 1; r < r_; ++r)
+                for (int j = 0; j < ns; ++j) {
+                    const long long q = ((long long)j * r) % L;
+                    const double ang = -2.0 * M_PI * (double)q / (double)L;
+                    host.push_back(make_float2((float)std::cos(ang), (float)std::sin(ang)));
+                }
+        }
+        ns *= r_;
+    }
+    if (host.empty()) host.push_back(make_float2(1.f, 0.f));
+    float2* d = nullptr;
+    HIP_TRY(hipMalloc(&d, host.size() * sizeof(float2)));
+    HIP_TRY(hipMemcpy(d, host.data(), host.size() * sizeof(float2), hipMemcpyHostToDevice));
+    g_twiddles[key] = d;
+    *out = d;
+    return 0;
+}
+
+__global__ void fill_int_kernel(int* p, int n, int v) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+
+// max(T) and sum(T^2) per hologram in double (np.amax(demanded_output),
+// src/algorithms.py:23; sum(T^2) is the constant term of the error expansion).
+template <typename TT>
+__global__ void __launch_bounds__(256) target_stats_kernel(const TT* tgt, long long holo, double* norm,
+                                                            float* normf, double* sum_t2) {
+    const int b = blockIdx.x;
+    const TT* p = tgt + (long long)b * holo;
+    double mx = 0.0, s2 = 0.0, d = 0.0;
+    for (long long i = threadIdx.x; i < holo; i += 256) {
+        const double v = (double)p[i];
+        mx = fmax(mx, v);
+        s2 += v * v;
+    }
+    block_reduce_stats<256>(mx, s2, d);
+    if (threadIdx.x == 0) {
+        norm[b] = mx;
+        normf[b] = (float)mx;
+        sum_t2[b] = s2;
+    }
+}
+
+}  // namespace
+
+struct slm_plan {
+    int algo = 0, B = 0, H = 0, W = 0, tt = 1, has_ain = 0, max_loops = 0;
+    int cw = 4, nwg = 0, col_threads = 0, row_threads = 0, rpw = 0;
+    int device = 0;
+    long long holo = 0;
+    hipStream_t stream = nullptr;
+    const float2* tw_row = nullptr;
+    const float2* tw_col = nullptr;
+    float2 *xa = nullptr, *xb = nullptr, *y = nullptr, *field = nullptr;
+    void* tgt = nullptr;
+    float* ain = nullptr;
+    float* phase_in = nullptr;
+    float* phase_out = nullptr;
+    float* e_out = nullptr;
+    double* partials = nullptr;
+    double* stats = nullptr;
+    int* stop = nullptr;
+    double* norm = nullptr;
+    float* normf = nullptr;
+    double* sum_t2 = nullptr;
+    float* lr = nullptr;
+    float* gather_buf = nullptr;
+    long long gather_elems = 0;
+    bool target_set = false, phase_set = false, field_set = false, lr_set = false;
+    // timing state (slm_plan_run_timed)
+    bool timing = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
+    std::vector<int> ev_class;
+    size_t ev_used = 0;
+};
+
+namespace {
+
+int pick_cw(int H, int W, int B) {
+    if (const char* s = std::getenv("SLM_COL_CW")) {
+        const int cw = std::atoi(s);
+        if (col_fn(H, cw, COL_GS_MAIN, TGT_F32) && W % cw == 0) return cw;
+    }
+    const int cands[3] = {16, 8, 4};
+    int best = 0;
+    for (int cw : cands) {
+        if (W % cw || !col_fn(H, cw, COL_GS_MAIN, TGT_F32)) continue;
+        if ((long long)(W / cw) * B >= 1024) return cw;
+        best = cw;  // keeps the smallest valid tile: most workgroups
+    }
+    return best;
+}
+
+int begin_launch(slm_plan* p, int cls) {
+    if (!p->timing) return 0;
+    if (p->ev_used == p->ev_pool.size()) {
+        hipEvent_t a, b;
+        HIP_TRY(hipEventCreate(&a));
+        HIP_TRY(hipEventCreate(&b));
+        p->ev_pool.emplace_back(a, b);
+        p->ev_class.push_back(cls);
+    }
+    p->ev_class[p->ev_used] = cls;
+    HIP_TRY(hipEventRecord(p->ev_pool[p->ev_used].first, p->stream));
+    return 0;
+}
+int end_launch(slm_plan* p) {
+    if (!p->timing) return 0;
+    HIP_TRY(hipEventRecord(p->ev_pool[p->ev_used].second, p->stream));
+    ++p->ev_used;
+    return 0;
+}
+
+RowParams row_params(slm_plan* p) {
+    RowParams r{};
+    r.ain = p->ain;
+    r.phase_in = p->phase_in;
+    r.phase_out = p->phase_out;
+    r.field = p->field;
+    r.lr = p->lr;
+    r.stop_iter = p->stop;
+    r.W = p->W;
+    r.holo = p->holo;
+    r.inv_s = (float)(1.0 / (double)p->holo);
+    r.tw = p->tw_row;
+    return r;
+}
+
+ColParams col_params(slm_plan* p) {
+    ColParams c{};
+    c.tgt = p->tgt;
+    c.partials = p->partials;
+    c.e_out = p->e_out;
+    c.stop_iter = p->stop;
+    c.norm = p->normf;
+    c.max_loops = p->max_loops;
+    c.W = p->W;
+    c.nwg = p->nwg;
+    c.holo = p->holo;
+    c.tw = p->tw_col;
+    return c;
+}
+
+int launch_row(slm_plan* p, int mode, const RowParams& rp, int cls) {
+    RowFn fn = row_fn(p->W, mode);
+    if (!fn) return fail(SLM_ERR_UNSUPPORTED, "no row kernel for width %d mode %d", p->W, mode);
+    int rc = begin_launch(p, cls);
+    if (rc) return rc;
+    hipLaunchKernelGGL(fn, dim3(p->H / p->rpw, p->B), dim3(p->row_threads), 0, p->stream, rp);
+    HIP_TRY(hipGetLastError());
+    return end_launch(p);
+}
+
+int launch_col(slm_plan* p, int mode, const ColParams& cp, int cls) {
+    const int tt = (mode == COL_EXPECTED || mode == COL_FFT_FWD || mode == COL_FFT_INV) ? TGT_F32 : p->tt;
+    ColFn fn = col_fn(p->H, p->cw, mode, tt);
+    if (!fn) return fail(SLM_ERR_UNSUPPORTED, "no column kernel for height %d cw %d mode %d", p->H, p->cw, mode);
+    int rc = begin_launch(p, cls);
+    if (rc) return rc;
+    hipLaunchKernelGGL(fn, dim3(p->nwg, p->B), dim3(p->col_threads), 0, p->stream, cp);
+    HIP_TRY(hipGetLastError());
+    return end_launch(p);
+}
+
+StatsParams stats_params(slm_plan* p, double tol) {
+    StatsParams s{};
+    s.partials = p->partials;
+    s.stats = p->stats;
+    s.stop_iter = p->stop;
+    s.norm = p->norm;
+    s.sum_t2 = p->sum_t2;
+    s.inv_s = 1.0 / (double)p->holo;
+    s.tol = tol;
+    s.max_loops = p->max_loops;
+    s.nwg = p->nwg;
+    return s;
+}
+
+int launch_finalize(slm_plan* p, double tol, int iter) {
+    StatsParams s = stats_params(p, tol);
+    s.iter = iter;
+    int rc = begin_launch(p, SLM_KERNEL_OTHER);
+    if (rc) return rc;
+    hipLaunchKernelGGL(stats_finalize_kernel, dim3(p->B), dim3(256), 0, p->stream, s);
+    HIP_TRY(hipGetLastError());
+    return end_launch(p);
+}
+
+#define RC(x)                 \
+    do {                      \
+        int rc_ = (x);        \
+        if (rc_) return rc_;  \
+    } while (0)
+
+int enqueue_gs(slm_plan* p, int loops, double tol, int checked) {
+    RowParams rp = row_params(p);
+    ColParams cp = col_params(p);
+    cp.loops = loops;
+    // setup: X0 = rowFFT(a_in A0/|A0|), A0 = ifft2(sqrt T) (src/algorithms.py:14-27),
+    // or the warm start B = a_in exp(i phi).
+    if (p->phase_set) {
+        rp.out = p->xa;
+        RC(launch_row(p, ROW_PHASE_FWD, rp, SLM_KERNEL_OTHER));
+    } else {
+        cp.out = p->y;
+        RC(launch_col(p, COL_REAL_INV, cp, SLM_KERNEL_OTHER));
+        rp.in = p->y;
+        rp.out = p->xa;
+        rp.iter = -1;
+        RC(launch_row(p, ROW_GS_MAIN, rp, SLM_KERNEL_OTHER));
+    }
+    for (int i = 0; i < loops; ++i) {
+        cp.in = p->xa;
+        cp.out = p->y;
+        cp.iter = i;
+        RC(launch_col(p, COL_GS_MAIN, cp, SLM_KERNEL_COL_MAIN));
+        if (checked) RC(launch_finalize(p, tol, i));
+        if (i + 1 < loops) {
+            rp.in = p->y;
+            rp.out = p->xa;
+            rp.iter = i;
+            RC(launch_row(p, ROW_GS_MAIN, rp, SLM_KERNEL_ROW_MAIN));
+        }
+    }
+    // hologram = np.angle(A) (src/algorithms.py:48); expected_outcome = |C|^2 (:36)
+    rp.in = p->y;
+    RC(launch_row(p, ROW_GS_PHASE, rp, SLM_KERNEL_OTHER));
+    cp.in = p->xa;
+    cp.in_alt = p->xa;
+    RC(launch_col(p, COL_EXPECTED, cp, SLM_KERNEL_OTHER));
+    return 0;
+}
+
+int enqueue_gd(slm_plan* p, int loops, double tol, int checked, float wa) {
+    RowParams rp = row_params(p);
+    ColParams cp = col_params(p);
+    cp.loops = loops;
+    cp.wa = wa;
+    // setup (make_initial_guess, src/algorithms.py:115-158): host-provided field
+    // or the "fourier" guess a_in exp(i angle(ifft2(sqrt T))).
+    if (p->field_set) {
+        rp.out = p->xa;
+        RC(launch_row(p, ROW_GD_INIT_FIELD, rp, SLM_KERNEL_OTHER));
+    } else {
+        cp.out = p->y;
+        RC(launch_col(p, COL_REAL_INV, cp, SLM_KERNEL_OTHER));
+        rp.in = p->y;
+        rp.out = p->xa;
+        RC(launch_row(p, ROW_GD_INIT_Y, rp, SLM_KERNEL_OTHER));
+    }
+    for (int i = 0; i < loops; ++i) {
+        float2* xi = (i & 1) ? p->xb : p->xa;
+        float2* xn = (i & 1) ? p->xa : p->xb;
+        cp.in = xi;
+        cp.iter = i;
+        RC(launch_col(p, COL_GD_STATS, cp, SLM_KERNEL_GD_STATS));
+        if (checked) RC(launch_finalize(p, tol, i));
+        cp.out = p->y;
+        RC(launch_col(p, COL_GD_GRAD, cp, SLM_KERNEL_COL_MAIN));
+        rp.in = p->y;
+        rp.out = xn;
+        rp.iter = i;
+        RC(launch_row(p, ROW_GD_MAIN, rp, SLM_KERNEL_ROW_MAIN));
+    }
+    {
+        int rc = begin_launch(p, SLM_KERNEL_OTHER);
+        if (rc) return rc;
+        const long long n = (long long)p->B * p->holo;
+        const int grid = (int)std::min<long long>(4096, (n + 255) / 256);
+        hipLaunchKernelGGL(field_phase_kernel, dim3(grid), dim3(256), 0, p->stream, (const float2*)p->field,
+                           p->phase_out, n);
+        HIP_TRY(hipGetLastError());
+        RC(end_launch(p));
+    }
+    cp.in = p->xa;
+    cp.in_alt = p->xb;
+    RC(launch_col(p, COL_EXPECTED, cp, SLM_KERNEL_OTHER));
+    return 0;
+}
+
+int enqueue_run(slm_plan* p, int loops, double tol, int checked, float wa) {
+    if (!p) return fail(SLM_ERR_ARG, "null plan");
+    if (!p->target_set) return fail(SLM_ERR_STATE, "target not set");
+    if (loops < 1 || loops > p->max_loops)
+        return fail(SLM_ERR_ARG, "loops %d outside [1, %d]", loops, p->max_loops);
+    if (p->algo == SLM_ALGO_GD && !p->lr_set) return fail(SLM_ERR_STATE, "learning rates not set");
+    HIP_TRY(hipSetDevice(p->device));
+    {
+        int rc = begin_launch(p, SLM_KERNEL_OTHER);
+        if (rc) return rc;
+        hipLaunchKernelGGL(fill_int_kernel, dim3((p->B + 255) / 256), dim3(256), 0, p->stream, p->stop, p->B,
+                           INT_MAX);
+        HIP_TRY(hipGetLastError());
+        RC(end_launch(p));
+    }
+    RC(p->algo == SLM_ALGO_GS ? enqueue_gs(p, loops, tol, checked) : enqueue_gd(p, loops, tol, checked, wa));
+    StatsParams s = stats_params(p, tol);
+    RC(begin_launch(p, SLM_KERNEL_OTHER));
+    hipLaunchKernelGGL(stats_reduce_kernel, dim3(loops, p->B), dim3(256), 0, p->stream, s);
+    HIP_TRY(hipGetLastError());
+    RC(end_launch(p));
+    return 0;
+}
+
+void free_plan(slm_plan* p) {
+    if (!p) return;
+    (void)hipSetDevice(p->device);
+    for (void* ptr : {(void*)p->xa, (void*)p->xb, (void*)p->y, (void*)p->field, p->tgt, (void*)p->ain,
+                      (void*)p->phase_in, (void*)p->phase_out, (void*)p->e_out, (void*)p->partials,
+                      (void*)p->stats, (void*)p->stop, (void*)p->norm, (void*)p->normf, (void*)p->sum_t2,
+                      (void*)p->lr, (void*)p->gather_buf})
+        if (ptr) (void)hipFree(ptr);
+    for (auto& e : p->ev_pool) {
+        (void)hipEventDestroy(e.first);
+        (void)hipEventDestroy(e.second);
+    }
+    if (p->stream) (void)hipStreamDestroy(p->stream);
+    delete p;
+}
+
+}  // namespace
+
+// ==========================================================================
+// C-ABI
+// ==========================================================================
+extern "C" {
+
+int slm_init(int device) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= 0)
+        return fail(SLM_ERR_HIP, "no HIP device available (%s); libslm_hip has no CPU path",
+                    hipGetErrorString(e));
+    if (device < 0 || device >= n) return fail(SLM_ERR_ARG, "device %d outside [0, %d)", device, n);
+    HIP_TRY(hipSetDevice(device));
+    g_device = device;
+    return 0;
+}
+
+int slm_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char* slm_last_error(void) { return g_err.c_str(); }
+
+const char* slm_version(void) { return "libslm_hip 0.1 (gfx950)"; }
+
+int slm_supported_length(int n) { return plan_index(n) >= 0 ? 1 : 0; }
+
+int slm_plan_create(int algo, int batch, int height, int width, int tgt_type, int has_ain, int max_loops,
+                    slm_plan** out) {
+    if (!out) return fail(SLM_ERR_ARG, "null output pointer");
+    *out = nullptr;
+    if (algo != SLM_ALGO_GS && algo != SLM_ALGO_GD) return fail(SLM_ERR_ARG, "unknown algorithm %d", algo);
+    if (batch < 1 || max_loops < 1) return fail(SLM_ERR_ARG, "batch and max_loops must be >= 1");
+    if (tgt_type != SLM_TGT_U8 && tgt_type != SLM_TGT_F32) return fail(SLM_ERR_ARG, "unknown target type");
+    if (!slm_supported_length(height) || !slm_supported_length(width))
+        return fail(SLM_ERR_UNSUPPORTED,
+                    "image shape %dx%d unsupported: each side must be one of 64, 128, 256, 512, 768, 1024, "
+                    "2048, 4096",
+                    height, width);
+    RC(ensure_device());
+    slm_plan* p = new slm_plan();
+    p->algo = algo;
+    p->B = batch;
+    p->H = height;
+    p->W = width;
+    p->tt = tgt_type;
+    p->has_ain = has_ain ? 1 : 0;
+    p->max_loops = max_loops;
+    p->device = g_device;
+    p->holo = (long long)height * width;
+    p->cw = pick_cw(height, width, batch);
+    if (!p->cw) {
+        delete p;
+        return fail(SLM_ERR_UNSUPPORTED, "no column tiling for %dx%d", height, width);
+    }
+    p->nwg = width / p->cw;
+    p->col_threads = col_threads(height, p->cw);
+    p->row_threads = row_threads(width);
+    p->rpw = row_rpw(width);
+    int rc = get_twiddles(width, &p->tw_row);
+    if (!rc) rc = get_twiddles(height, &p->tw_col);
+    if (rc) {
+        delete p;
+        return rc;
+    }
+    const size_t n = (size_t)batch * p->holo;
+    const size_t tb = tgt_type == SLM_TGT_U8 ? 1 : 4;
+    auto alloc = [&](void** ptr, size_t bytes) -> int {
+        hipError_t e = hipMalloc(ptr, bytes);
+        if (e != hipSuccess) {
+            free_plan(p);
+            return fail(SLM_ERR_HIP, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+        }
+        return 0;
+    };
+    hipError_t se = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking);
+    if (se != hipSuccess) {
+        delete p;
+        return fail(SLM_ERR_HIP, "stream creation failed: %s", hipGetErrorString(se));
+    }
+    RC(alloc((void**)&p->xa, n * sizeof(float2)));
+    RC(alloc((void**)&p->y, n * sizeof(float2)));
+    if (algo == SLM_ALGO_GD) {
+        RC(alloc((void**)&p->xb, n * sizeof(float2)));
+        RC(alloc((void**)&p->field, n * sizeof(float2)));
+        RC(alloc((void**)&p->lr, (size_t)max_loops * sizeof(float)));
+    }
+    RC(alloc(&p->tgt, n * tb));
+    if (has_ain) RC(alloc((void**)&p->ain, (size_t)p->holo * sizeof(float)));
+    RC(alloc((void**)&p->phase_out, n * sizeof(float)));
+    RC(alloc((void**)&p->e_out, n * sizeof(float)));
+    RC(alloc((void**)&p->partials, (size_t)batch * max_loops * p->nwg * 4 * sizeof(double)));
+    RC(alloc((void**)&p->stats, (size_t)batch * max_loops * 4 * sizeof(double)));
+    RC(alloc((void**)&p->stop, (size_t)batch * sizeof(int)));
+    RC(alloc((void**)&p->norm, (size_t)batch * sizeof(double)));
+    RC(alloc((void**)&p->normf, (size_t)batch * sizeof(float)));
+    RC(alloc((void**)&p->sum_t2, (size_t)batch * sizeof(double)));
+    *out = p;
+    return 0;
+}
+
+int slm_plan_destroy(slm_plan* plan) {
+    free_plan(plan);
+    return 0;
+}
+
+int slm_plan_set_target(slm_plan* p, const void* tgt) {
+    if (!p || !tgt) return fail(SLM_ERR_ARG, "null argument");
+    HIP_TRY(hipSetDevice(p->device));
+    const size_t tb = p->tt == SLM_TGT_U8 ? 1 : 4;
+    HIP_TRY(hipMemcpyAsync(p->tgt, tgt, (size_t)p->B * p->holo * tb, hipMemcpyHostToDevice, p->stream));
+    if (p->tt == SLM_TGT_U8)
+        hipLaunchKernelGGL(target_stats_kernel<uint8_t>, dim3(p->B), dim3(256), 0, p->stream,
+                           (const uint8_t*)p->tgt, p->holo, p->norm, p->normf, p->sum_t2);
+    else
+        hipLaunchKernelGGL(target_stats_kernel<float>, dim3(p->B), dim3(256), 0, p->stream, (const float*)p->tgt,
+                           p->holo, p->norm, p->normf, p->sum_t2);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(p->stream));
+    p->target_set = true;
+    return 0;
+}
+
+int slm_plan_set_ain(slm_plan* p, const float* ain) {
+    if (!p || !ain) return fail(SLM_ERR_ARG, "null argument");
+    if (!p->has_ain) return fail(SLM_ERR_STATE, "plan was created without an incoming amplitude");
+    HIP_TRY(hipSetDevice(p->device));
+    HIP_TRY(hipMemcpy(p->ain, ain, (size_t)p->holo * sizeof(float), hipMemcpyHostToDevice));
+    return 0;
+}
+
+int slm_plan_set_phase(slm_plan* p, const float* phase) {
+    if (!p) return fail(SLM_ERR_ARG, "null plan");
+    if (p->algo != SLM_ALGO_GS) return fail(SLM_ERR_STATE, "initial phase applies to GS plans");
+    HIP_TRY(hipSetDevice(p->device));
+    if (!phase) {
+        p->phase_set = false;
+        return 0;
+    }
+    const size_t bytes = (size_t)p->B * p->holo * sizeof(float);
+    if (!p->phase_in) HIP_TRY(hipMalloc((void**)&p->phase_in, bytes));
+    HIP_TRY(hipMemcpy(p->phase_in, phase, bytes, hipMemcpyHostToDevice));
+    p->phase_set = true;
+    return 0;
+}
+
+int slm_plan_set_field(slm_plan* p, const float* field) {
+    if (!p) return fail(SLM_ERR_ARG, "null plan");
+    if (p->algo != SLM_ALGO_GD) return fail(SLM_ERR_STATE, "initial field applies to GD plans");
+    HIP_TRY(hipSetDevice(p->device));
+    if (!field) {
+        p->field_set = false;
+        return 0;
+    }
+    HIP_TRY(hipMemcpy(p->field, field, (size_t)p->B * p->holo * sizeof(float2), hipMemcpyHostToDevice));
+    p->field_set = true;
+    return 0;
+}
+
+int slm_plan_set_lr(slm_plan* p, const float* lr) {
+    if (!p || !lr) return fail(SLM_ERR_ARG, "null argument");
+    if (p->algo != SLM_ALGO_GD) return fail(SLM_ERR_STATE, "learning rates apply to GD plans");
+    HIP_TRY(hipSetDevice(p->device));
+    HIP_TRY(hipMemcpy(p->lr, lr, (size_t)p->max_loops * sizeof(float), hipMemcpyHostToDevice));
+    p->lr_set = true;
+    return 0;
+}
+
+int slm_plan_run(slm_plan* p, int loops, double tol, int checked, float wa) {
+    if (p) p->timing = false;
+    return enqueue_run(p, loops, tol, checked, wa);
+}
+
+int slm_plan_run_timed(slm_plan* p, int loops, double tol, int checked, float wa, double* us, int* counts) {
+    if (!p) return fail(SLM_ERR_ARG, "null plan");
+    p->timing = true;
+    p->ev_used = 0;
+    int rc = enqueue_run(p, loops, tol, checked, wa);
+    p->timing = false;
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(p->stream));
+    for (int k = 0; k < SLM_NUM_KERNEL_CLASSES; ++k) {
+        if (us) us[k] = 0.0;
+        if (counts) counts[k] = 0;
+    }
+    for (size_t i = 0; i < p->ev_used; ++i) {
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, p->ev_pool[i].first, p->ev_pool[i].second));
+        const int c = p->ev_class[i];
+        if (us) us[c] += 1000.0 * ms;
+        if (counts) counts[c] += 1;
+    }
+    return 0;
+}
+
+int slm_plan_sync(slm_plan* p) {
+    if (!p) return fail(SLM_ERR_ARG, "null plan");
+    HIP_TRY(hipSetDevice(p->device));
+    HIP_TRY(hipStreamSynchronize(p->stream));
+    return 0;
+}
+
+int slm_plan_read(slm_plan* p, float* phase, float* expected, double* stats, int* iters) {
+    if (!p) return fail(SLM_ERR_ARG, "null plan");
+    HIP_TRY(hipSetDevice(p->device));
+    HIP_TRY(hipStreamSynchronize(p->stream));
+    const size_t n = (size_t)p->B * p->holo;
+    if (phase) HIP_TRY(hipMemcpy(phase, p->phase_out, n * sizeof(float), hipMemcpyDeviceToHost));
+    if (expected) HIP_TRY(hipMemcpy(expected, p->e_out, n * sizeof(float), hipMemcpyDeviceToHost));
+    if (stats)
+        HIP_TRY(hipMemcpy(stats, p->stats, (size_t)p->B * p->max_loops * 4 * sizeof(double),
+                          hipMemcpyDeviceToHost));
+    if (iters) {
+        std::vector<int> st(p->B);
+        HIP_TRY(hipMemcpy(st.data(), p->stop, (size_t)p->B * sizeof(int), hipMemcpyDeviceToHost));
+        for (int b = 0; b < p->B; ++b) iters[b] = st[b] == INT_MAX ? -1 : st[b] + 1;  // -1: ran all loops
+    }
+    return 0;
+}
+
+int slm_plan_read_target_stats(slm_plan* p, double* norm, double* sum_t2) {
+    if (!p) return fail(SLM_ERR_ARG, "null plan");
+    HIP_TRY(hipSetDevice(p->device));
+    HIP_TRY(hipStreamSynchronize(p->stream));
+    if (norm) HIP_TRY(hipMemcpy(norm, p->norm, (size_t)p->B * sizeof(double), hipMemcpyDeviceToHost));
+    if (sum_t2) HIP_TRY(hipMemcpy(sum_t2, p->sum_t2, (size_t)p->B * sizeof(double), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+long long slm_plan_kernel_bytes(slm_plan* p, int cls) {
+    if (!p) return -1;
+    const long long px = (long long)p->B * p->holo;
+    const long long tb = p->tt == SLM_TGT_U8 ? 1 : 4;
+    const long long ab = p->has_ain ? 4 : 0;
+    switch (cls) {
+        case SLM_KERNEL_COL_MAIN: return px * (8 + tb + 8);       // X in, T in, Y out
+        case SLM_KERNEL_ROW_MAIN:                                 // Y in, X out (+ a_in) (+ field r/w for GD)
+            return px * (16 + ab + (p->algo == SLM_ALGO_GD ? 16 : 0));
+        case SLM_KERNEL_GD_STATS: return px * (8 + tb);           // X in, T in
+        default: return 0;
+    }
+}
+
+int slm_plan_info(slm_plan* p, int* info) {
+    if (!p || !info) return fail(SLM_ERR_ARG, "null argument");
+    info[0] = p->cw;
+    info[1] = p->nwg;
+    info[2] = p->col_threads;
+    info[3] = p->row_threads;
+    info[4] = p->rpw;
+    return 0;
+}
+
+int slm_gs(const void* tgt, int tgt_type, const float* ain, int batch, int height, int width, int max_loops,
+           double tol, const float* init_phase, float* out_phase, float* out_expected, double* out_stats,
+           int* out_iters) {
+    slm_plan* p = nullptr;
+    RC(slm_plan_create(SLM_ALGO_GS, batch, height, width, tgt_type, ain != nullptr, max_loops, &p));
+    int rc = slm_plan_set_target(p, tgt);
+    if (!rc && ain) rc = slm_plan_set_ain(p, ain);
+    if (!rc && init_phase) rc = slm_plan_set_phase(p, init_phase);
+    if (!rc) rc = slm_plan_run(p, max_loops, tol, tol > 0.0 ? 1 : 0, 0.f);
+    if (!rc) rc = slm_plan_read(p, out_phase, out_expected, out_stats, out_iters);
+    free_plan(p);
+    return rc;
+}
+
+int slm_gd(const void* tgt, int tgt_type, const float* ain, int batch, int height, int width, int max_loops,
+           double tol, const float* init_field, const float* lr, float wa, float* out_phase, float* out_expected,
+           double* out_stats, int* out_iters) {
+    slm_plan* p = nullptr;
+    RC(slm_plan_create(SLM_ALGO_GD, batch, height, width, tgt_type, ain != nullptr, max_loops, &p));
+    int rc = slm_plan_set_target(p, tgt);
+    if (!rc && ain) rc = slm_plan_set_ain(p, ain);
+    if (!rc && init_field) rc = slm_plan_set_field(p, init_field);
+    if (!rc) rc = slm_plan_set_lr(p, lr);
+    if (!rc) rc = slm_plan_run(p, max_loops, tol, tol > 0.0 ? 1 : 0, wa);
+    if (!rc) rc = slm_plan_read(p, out_phase, out_expected, out_stats, out_iters);
+    free_plan(p);
+    return rc;
+}
+
+int slm_fft2(const float* in, float* out, int batch, int height, int width, int inverse) {
+    if (!in || !out) return fail(SLM_ERR_ARG, "null argument");
+    slm_plan* p = nullptr;
+    RC(slm_plan_create(SLM_ALGO_GS, batch, height, width, SLM_TGT_F32, 0, 1, &p));
+    const size_t bytes = (size_t)batch * p->holo * sizeof(float2);
+    int rc = 0;
+    hipError_t e = hipMemcpy(p->xa, in, bytes, hipMemcpyHostToDevice);
+    if (e != hipSuccess) rc = fail(SLM_ERR_HIP, "upload failed: %s", hipGetErrorString(e));
+    if (!rc) {
+        RowParams rp = row_params(p);
+        rp.in = p->xa;
+        rp.out = p->y;
+        rc = launch_row(p, inverse ? ROW_FFT_INV : ROW_FFT_FWD, rp, SLM_KERNEL_OTHER);
+    }
+    if (!rc) {
+        ColParams cp = col_params(p);
+        cp.in = p->y;
+        cp.out = p->xa;
+        rc = launch_col(p, inverse ? COL_FFT_INV : COL_FFT_FWD, cp, SLM_KERNEL_OTHER);
+    }
+    if (!rc) {
+        e = hipStreamSynchronize(p->stream);
+        if (e == hipSuccess) e = hipMemcpy(out, p->xa, bytes, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) rc = fail(SLM_ERR_HIP, "fft2 failed: %s", hipGetErrorString(e));
+    }
+    free_plan(p);
+    return rc;
+}
+
+int slm_comm_unique_id(unsigned char* id128) {
+    if (!id128) return fail(SLM_ERR_ARG, "null argument");
+    ncclUniqueId id;
+    NCCL_TRY(ncclGetUniqueId(&id));
+    std::memcpy(id128, id.internal, NCCL_UNIQUE_ID_BYTES);
+    return 0;
+}
+
+int slm_comm_init(int nranks, int rank, const unsigned char* id128) {
+    if (!id128 || nranks < 1 || rank < 0 || rank >= nranks) return fail(SLM_ERR_ARG, "bad communicator arguments");
+    RC(ensure_device());
+    if (g_comm) {
+        ncclCommDestroy(g_comm);
+        g_comm = nullptr;
+    }
+    ncclUniqueId id;
+    std::memcpy(id.internal, id128, NCCL_UNIQUE_ID_BYTES);
+    NCCL_TRY(ncclCommInitRank(&g_comm, nranks, id, rank));
+    g_comm_rank = rank;
+    g_comm_size = nranks;
+    return 0;
+}
+
+int slm_comm_destroy(void) {
+    if (g_comm) {
+        ncclCommDestroy(g_comm);
+        g_comm = nullptr;
+    }
+    return 0;
+}
+
+int slm_plan_gather_phase(slm_plan* p, const int* counts, int root, float* host_out) {
+    if (!p || !counts) return fail(SLM_ERR_ARG, "null argument");
+    HIP_TRY(hipSetDevice(p->device));
+    const int n = g_comm ? g_comm_size : 1;
+    const int me = g_comm ? g_comm_rank : 0;
+    if (counts[me] != p->B) return fail(SLM_ERR_ARG, "counts[%d]=%d but the plan holds %d", me, counts[me], p->B);
+    long long total = 0;
+    for (int r = 0; r < n; ++r) total += counts[r];
+    if (me == root) {
+        const long long elems = total * p->holo;
+        if (p->gather_elems < elems) {
+            if (p->gather_buf) HIP_TRY(hipFree(p->gather_buf));
+            HIP_TRY(hipMalloc((void**)&p->gather_buf, elems * sizeof(float)));
+            p->gather_elems = elems;
+        }
+        long long off = 0;
+        if (n > 1) NCCL_TRY(ncclGroupStart());
+        for (int r = 0; r < n; ++r) {
+            const size_t cnt = (size_t)counts[r] * p->holo;
+            if (r == me) {
+                HIP_TRY(hipMemcpyAsync(p->gather_buf + off, p->phase_out, cnt * sizeof(float),
+                                       hipMemcpyDeviceToDevice, p->stream));
+            } else if (cnt) {
+                NCCL_TRY(ncclRecv(p->gather_buf + off, cnt, ncclFloat32, r, g_comm, p->stream));
+            }
+            off += (long long)counts[r] * p->holo;
+        }
+        if (n > 1) NCCL_TRY(ncclGroupEnd());
+        HIP_TRY(hipStreamSynchronize(p->stream));
+        if (host_out)
+            HIP_TRY(hipMemcpy(host_out, p->gather_buf, (size_t)elems * sizeof(float), hipMemcpyDeviceToHost));
+    } else {
+        if (!g_comm) return fail(SLM_ERR_COMM, "no communicator");
+        if (p->B)
+            NCCL_TRY(ncclSend(p->phase_out, (size_t)p->B * p->holo, ncclFloat32, root, g_comm, p->stream));
+        HIP_TRY(hipStreamSynchronize(p->stream));
+    }
+    return 0;
+}
+
+}  // extern "C"
