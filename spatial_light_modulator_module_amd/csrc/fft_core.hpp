@@ -51,6 +51,9 @@ struct PlanOf {
     static constexpr int E = kPlans[plan_index(N)].e;
     static constexpr int T = N / E;
     static constexpr int LINE = lds_line(N);
+    // row stride of per-row LDS regions: == 16 (mod 32) complex, so the two rows
+    // served by one 32-lane ds_read_b64 group hit disjoint halves of the banks
+    static constexpr int ROWSTRIDE = LINE + ((16 - LINE % 32) + 32) % 32;
 };
 
 // cos(2 pi q / 48) for the constant twiddles of radix 2, 3, 4, 8, 12, 16.
@@ -223,13 +226,89 @@ struct LdsTile {  // CW interleaved columns (column kernels): [o][c]
 };
 
 // ------------------------------------------------------------------------
-// Stockham driver. v[m] holds element t + T m on entry (any order of the
-// line's data in the slot layout) and the transform's element t + T m on exit.
-// Twiddles of the passes after the first come from the per-length table
-// `tw` (forward convention; conjugated here for the inverse).
+// Per-thread twiddles. Which twiddles a thread needs depends only on its
+// transform-thread index t, so they are loaded once per kernel (one global
+// load each, table computed in double on the host) and shared by every
+// transform the thread runs (inverse and forward use conjugates).
 // ------------------------------------------------------------------------
-template <int N, int E, bool INV, int Ns, int TwOff, class Lds, int R, int... Rest>
-__device__ __forceinline__ void stockham_pass(float2 (&v)[E], int t, const float2* __restrict__ tw, const Lds& lds) {
+template <int N, int Ns, int... Rs>
+struct TwCountImpl;
+template <int N, int Ns>
+struct TwCountImpl<N, Ns> {
+    static constexpr int value = 0;
+};
+template <int N, int Ns, int R, int... Rest>
+struct TwCountImpl<N, Ns, R, Rest...> {
+    static constexpr int value = (Ns > 1 ? (PlanOf<N>::E / R) * (R - 1) : 0) + TwCountImpl<N, Ns * R, Rest...>::value;
+};
+template <int N, class L>
+struct TwCountOf;
+template <int N, int... Rs>
+struct TwCountOf<N, IntList<Rs...>> {
+    static constexpr int value = TwCountImpl<N, 1, Rs...>::value;
+};
+
+// CACHED: every twiddle of the thread in registers (one load each per kernel).
+// !CACHED: read from the (L1/L2-resident) table where used — for 1024-thread
+// workgroups whose 128-VGPR budget cannot hold the cache.
+template <int N, bool CACHED = true>
+struct Twiddles {
+    static constexpr int COUNT = TwCountOf<N, RadicesOf<N>>::value > 0 ? TwCountOf<N, RadicesOf<N>>::value : 1;
+    float2 w[COUNT];
+    template <int TwOff, int RegOff, int R, int Ns>
+    __device__ __forceinline__ float2 get(int k, int r, int j) const {
+        return w[RegOff + k * (R - 1) + r - 1];
+    }
+};
+template <int N>
+struct Twiddles<N, false> {
+    const float2* __restrict__ table;
+    template <int TwOff, int RegOff, int R, int Ns>
+    __device__ __forceinline__ float2 get(int k, int r, int j) const {
+        return table[TwOff + (r - 1) * Ns + j];
+    }
+};
+
+template <int N, int E, int Ns, int TwOff, int RegOff, int R, int... Rest>
+__device__ __forceinline__ void load_twiddles_pass(Twiddles<N, true>& tw, int t, const float2* __restrict__ table) {
+    constexpr int T = N / E;
+    constexpr int NB = E / R;
+    if constexpr (Ns > 1) {
+        static_for<NB>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            const int j = (t + k * T) % Ns;
+            static_for<R - 1>([&](auto rc) {
+                constexpr int r = decltype(rc)::value;
+                tw.w[RegOff + k * (R - 1) + r] = table[TwOff + r * Ns + j];
+            });
+        });
+    }
+    if constexpr (sizeof...(Rest) > 0) {
+        constexpr int kNextOff = TwOff + (Ns > 1 ? (R - 1) * Ns : 0);
+        constexpr int kNextReg = RegOff + (Ns > 1 ? NB * (R - 1) : 0);
+        load_twiddles_pass<N, E, Ns * R, kNextOff, kNextReg, Rest...>(tw, t, table);
+    }
+}
+template <int N, int... Rs>
+__device__ __forceinline__ void load_twiddles_impl(Twiddles<N, true>& tw, int t, const float2* table,
+                                                   IntList<Rs...>) {
+    load_twiddles_pass<N, PlanOf<N>::E, 1, 0, 0, Rs...>(tw, t, table);
+}
+template <int N>
+__device__ __forceinline__ void load_twiddles(Twiddles<N, true>& tw, int t, const float2* __restrict__ table) {
+    load_twiddles_impl<N>(tw, t, table, RadicesOf<N>{});
+}
+template <int N>
+__device__ __forceinline__ void load_twiddles(Twiddles<N, false>& tw, int, const float2* __restrict__ table) {
+    tw.table = table;
+}
+
+// ------------------------------------------------------------------------
+// Stockham driver. v[m] holds element t + T m on entry and the transform's
+// element t + T m on exit.
+// ------------------------------------------------------------------------
+template <int N, int E, bool INV, int Ns, int TwOff, int RegOff, class Lds, class Tw, int R, int... Rest>
+__device__ __forceinline__ void stockham_pass(float2 (&v)[E], int t, const Tw& tw, const Lds& lds) {
     constexpr int T = N / E;
     constexpr int NB = E / R;
     static_assert(E % R == 0, "radix must divide elements per thread");
@@ -245,7 +324,7 @@ __device__ __forceinline__ void stockham_pass(float2 (&v)[E], int t, const float
         if constexpr (Ns > 1) {
             static_for<R - 1>([&](auto rc) {
                 constexpr int r = decltype(rc)::value + 1;
-                const float2 w = tw[TwOff + (r - 1) * Ns + j];
+                const float2 w = tw.template get<TwOff, RegOff, R, Ns>(k, r, j);
                 u[r] = INV ? cmulc(u[r], w) : cmul(u[r], w);
             });
         }
@@ -271,22 +350,22 @@ __device__ __forceinline__ void stockham_pass(float2 (&v)[E], int t, const float
             v[m] = lds.load(t + m * T);
         });
         __syncthreads();
+        constexpr int kNextReg = RegOff + (Ns > 1 ? NB * (R - 1) : 0);
         constexpr int kNextOff = TwOff + (Ns > 1 ? (R - 1) * Ns : 0);
-        stockham_pass<N, E, INV, Ns * R, kNextOff, Lds, Rest...>(v, t, tw, lds);
+        stockham_pass<N, E, INV, Ns * R, kNextOff, kNextReg, Lds, Tw, Rest...>(v, t, tw, lds);
     }
 }
 
-template <int N, bool INV, class Lds, int... Rs>
-__device__ __forceinline__ void fft_line_impl(float2 (&v)[PlanOf<N>::E], int t, const float2* __restrict__ tw,
-                                              const Lds& lds, IntList<Rs...>) {
-    stockham_pass<N, PlanOf<N>::E, INV, 1, 0, Lds, Rs...>(v, t, tw, lds);
+template <int N, bool INV, class Lds, class Tw, int... Rs>
+__device__ __forceinline__ void fft_line_impl(float2 (&v)[PlanOf<N>::E], int t, const Tw& tw, const Lds& lds,
+                                              IntList<Rs...>) {
+    stockham_pass<N, PlanOf<N>::E, INV, 1, 0, 0, Lds, Tw, Rs...>(v, t, tw, lds);
 }
 
 // Transform one line held in the slot layout. Every thread of the workgroup
 // must call this (it contains workgroup barriers).
-template <int N, bool INV, class Lds>
-__device__ __forceinline__ void fft_line(float2 (&v)[PlanOf<N>::E], int t, const float2* __restrict__ tw,
-                                         const Lds& lds) {
+template <int N, bool INV, class Lds, class Tw>
+__device__ __forceinline__ void fft_line(float2 (&v)[PlanOf<N>::E], int t, const Tw& tw, const Lds& lds) {
     fft_line_impl<N, INV>(v, t, tw, lds, RadicesOf<N>{});
 }
 

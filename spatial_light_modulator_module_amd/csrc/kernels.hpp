@@ -39,6 +39,7 @@ struct RowParams {
     const int* stop_iter;    // [B], INT_MAX while running
     int iter;                // iteration index of this launch
     int W;                   // row length (== template W; kept for checks)
+    int H;                   // rows per hologram (column stride of the blocked layout)
     long long holo;          // elements per hologram (H * W)
     float inv_s;             // 1 / (H * W)
     const float2* tw;        // twiddle table for length W
@@ -99,7 +100,7 @@ using ColFn = void (*)(ColParams);
 template <int W>
 struct RowCfg {
     static constexpr int T = PlanOf<W>::T;
-    static constexpr int RPW = (T >= 256) ? 1 : 256 / T;  // rows per workgroup
+    static constexpr int RPW = (T >= 64) ? 4 : 256 / T;  // rows per workgroup, a multiple of 4
     static constexpr int THREADS = RPW * T;
 };
 
@@ -120,15 +121,30 @@ __device__ __forceinline__ int xcd_remap(int id, int n) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
 }
 
+// Internal layout of the iteration state (X, Y, GD field, device target):
+// 4-column blocks, [x / 4][y][x % 4]. A 4-column panel is one contiguous run
+// (column pass), and rows y..y+3 (y % 4 == 0) of a block form one 128-B line
+// (row pass on row quads), so both passes move whole lines. User-facing
+// arrays (phases, a_in, expected output) stay row-major.
+__host__ __device__ __forceinline__ long long blk_index(long long y, int x, int H) {
+    return (((long long)(x >> 2) * H + y) << 2) + (x & 3);
+}
+
 // ------------------------------------------------------------------------
 // element-wise pieces
 // ------------------------------------------------------------------------
 // a * z / |z|, with angle(0) = 0 -> a (np.angle(0) == 0, src/algorithms.py:30,33).
+// 1/sqrt(n2) to ~0.5 ulp: hardware estimate plus one Newton step (the
+// projection runs every iteration, so its rounding accumulates).
+__device__ __forceinline__ float rsqrt_nr(float n2) {
+    const float r = rsqrtf(n2);
+    return fmaf(r * 0.5f, fmaf(-n2 * r, r, 1.0f), r);
+}
 __device__ __forceinline__ float2 unit_scale(float2 z, float a) {
     const float n2 = z.x * z.x + z.y * z.y;
-    if (n2 == 0.0f) return make_float2(a, 0.0f);
-    const float r = a * rsqrtf(n2);
-    return make_float2(z.x * r, z.y * r);
+    const bool zero = (n2 == 0.0f);  // select, not branch: no divergence in the unrolled loops
+    const float r = a * rsqrt_nr(zero ? 1.0f : n2);
+    return make_float2(zero ? a : z.x * r, zero ? 0.0f : z.y * r);
 }
 
 template <int TT>
@@ -184,21 +200,29 @@ __global__ void __launch_bounds__(RowCfg<W>::THREADS) row_kernel(RowParams p) {
     constexpr int E = PlanOf<W>::E;
     constexpr int T = PlanOf<W>::T;
     constexpr int RPW = RowCfg<W>::RPW;
-    constexpr int LINE = PlanOf<W>::LINE;
+    constexpr int LINE = PlanOf<W>::ROWSTRIDE;
+    constexpr int TL = T < 16 ? T : 16;
     __shared__ float2 smem[RPW * LINE];
 
     const int b = blockIdx.y;
-    if constexpr (MODE == ROW_GS_MAIN) {
-        if (p.iter >= p.stop_iter[b]) return;  // stopped after this iteration's column pass
-    } else if constexpr (MODE == ROW_GD_MAIN) {
-        if (p.iter > p.stop_iter[b]) return;
-    }
-    const int q = threadIdx.x / T;
-    const int t = threadIdx.x - q * T;
-    const int row = blockIdx.x * RPW + q;
-    const long long roff = (long long)row * W;
-    const long long off = (long long)b * p.holo + roff;
-    const LdsLine lds{smem + q * LINE};
+    // lane -> (row within the quad, transform thread t): TL consecutive t of
+    // one row, then the next row of the quad. One wave instruction touches
+    // 16 consecutive x of 4 rows = four whole 128-B lines of the blocked layout,
+    // and a 16-lane LDS write group stays inside one row.
+    const int tlo = threadIdx.x % TL;
+    const int q4 = (threadIdx.x / TL) & 3;
+    const int rest = threadIdx.x / (4 * TL);
+    const int qq = rest / (T / TL);
+    const int t = tlo + TL * (rest - qq * (T / TL));
+    const int lrow = qq * 4 + q4;
+    const int row = blockIdx.x * RPW + lrow;
+    const long long hoff = (long long)b * p.holo;
+    const long long roff = (long long)row * W;                  // row-major (user arrays)
+    const long long boff = hoff + blk_index(row, t, p.H);        // blocked (state), slot m adds m*T*H
+    const long long bstep = (long long)T * p.H;
+    const LdsLine lds{smem + lrow * LINE};
+    Twiddles<W, (RowCfg<W>::THREADS <= 512)> tw;
+    load_twiddles<W>(tw, t, p.tw);
     float2 v[E];
 
     auto ain_at = [&](int m) -> float { return p.ain ? p.ain[roff + t + T * m] : 1.0f; };
@@ -207,35 +231,41 @@ __global__ void __launch_bounds__(RowCfg<W>::THREADS) row_kernel(RowParams p) {
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             float s, c;
-            sincosf(p.phase_in[off + t + T * m], &s, &c);
+            sincosf(p.phase_in[hoff + roff + t + T * m], &s, &c);
             const float a = ain_at(m);
             v[m] = make_float2(a * c, a * s);
         }
     } else if constexpr (MODE == ROW_GD_INIT_FIELD) {
 #pragma unroll
         for (int m = 0; m < E; ++m) {
-            const float2 x = p.field[off + t + T * m];
+            const float2 x = p.field[boff + m * bstep];
             const float a = ain_at(m);
-            const float r = rsqrtf(x.x * x.x + x.y * x.y);
+            const float r = rsqrt_nr(x.x * x.x + x.y * x.y);
             v[m] = make_float2(x.x * r * a, x.y * r * a);
         }
     } else {
 #pragma unroll
-        for (int m = 0; m < E; ++m) v[m] = p.in[off + t + T * m];
+        for (int m = 0; m < E; ++m) v[m] = p.in[boff + m * bstep];
+    }
+    // the stop test is issued behind the loads so its latency overlaps them
+    if constexpr (MODE == ROW_GS_MAIN) {
+        if (p.iter >= p.stop_iter[b]) return;  // stopped after this iteration's column pass
+    } else if constexpr (MODE == ROW_GD_MAIN) {
+        if (p.iter > p.stop_iter[b]) return;
     }
 
     if constexpr (MODE == ROW_GS_MAIN || MODE == ROW_GS_PHASE || MODE == ROW_GD_INIT_Y || MODE == ROW_GD_MAIN ||
                   MODE == ROW_FFT_INV) {
-        fft_line<W, true>(v, t, p.tw, lds);
+        fft_line<W, true>(v, t, tw, lds);
     }
 
     if constexpr (MODE == ROW_GS_PHASE) {
 #pragma unroll
-        for (int m = 0; m < E; ++m) p.phase_out[off + t + T * m] = atan2f(v[m].y, v[m].x);
+        for (int m = 0; m < E; ++m) p.phase_out[hoff + roff + t + T * m] = atan2f(v[m].y, v[m].x);
         return;
     } else if constexpr (MODE == ROW_FFT_INV) {
 #pragma unroll
-        for (int m = 0; m < E; ++m) p.out[off + t + T * m] = v[m];
+        for (int m = 0; m < E; ++m) p.out[boff + m * bstep] = v[m];
         return;
     } else {
         if constexpr (MODE == ROW_GS_MAIN) {
@@ -246,8 +276,8 @@ __global__ void __launch_bounds__(RowCfg<W>::THREADS) row_kernel(RowParams p) {
             for (int m = 0; m < E; ++m) {
                 const float a = ain_at(m);
                 const float2 x = unit_scale(v[m], a);  // a_in exp(i angle(ifft2(sqrt T)))
-                p.field[off + t + T * m] = x;
-                const float r = rsqrtf(x.x * x.x + x.y * x.y);
+                p.field[boff + m * bstep] = x;
+                const float r = rsqrt_nr(x.x * x.x + x.y * x.y);
                 v[m] = make_float2(x.x * r * a, x.y * r * a);
             }
         } else if constexpr (MODE == ROW_GD_MAIN) {
@@ -258,7 +288,7 @@ __global__ void __launch_bounds__(RowCfg<W>::THREADS) row_kernel(RowParams p) {
             for (int m = 0; m < E; ++m) {
                 const float a = ain_at(m);
                 const float2 g = make_float2(v[m].x * p.inv_s * a, v[m].y * p.inv_s * a);
-                const long long idx = off + t + T * m;
+                const long long idx = boff + m * bstep;
                 float2 x = p.field[idx];
                 const float ax2 = x.x * x.x + x.y * x.y;
                 const float inv = 1.0f / sqrtf(ax2);
@@ -269,13 +299,13 @@ __global__ void __launch_bounds__(RowCfg<W>::THREADS) row_kernel(RowParams p) {
                 x.x -= lr * dx;
                 x.y -= lr * dy;
                 p.field[idx] = x;
-                const float r = rsqrtf(x.x * x.x + x.y * x.y);
+                const float r = rsqrt_nr(x.x * x.x + x.y * x.y);
                 v[m] = make_float2(x.x * r * a, x.y * r * a);
             }
         }
-        fft_line<W, false>(v, t, p.tw, lds);
+        fft_line<W, false>(v, t, tw, lds);
 #pragma unroll
-        for (int m = 0; m < E; ++m) p.out[off + t + T * m] = v[m];
+        for (int m = 0; m < E; ++m) p.out[boff + m * bstep] = v[m];
     }
 }
 
@@ -291,15 +321,16 @@ __global__ void __launch_bounds__((ColCfg<H, CW>::THREADS)) col_kernel(ColParams
     __shared__ float2 smem[LINE * CW];
 
     const int b = blockIdx.y;
-    if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_STATS || MODE == COL_GD_GRAD) {
-        if (p.iter > p.stop_iter[b]) return;
-    }
     const int wg = xcd_remap(blockIdx.x, gridDim.x);
     const int c = threadIdx.x % CW;
     const int t = threadIdx.x / CW;
     const int x = wg * CW + c;
-    const long long base = (long long)b * p.holo + x;
+    // blocked layout: element (y, x) at blk_index(y, x, H); row y = t + T m
+    const long long base = (long long)b * p.holo + blk_index(t, x, H);
+    constexpr long long kStep = 4LL * T;
     const LdsTile<CW> lds{smem, c};
+    Twiddles<H, (THREADS <= 512)> tw;
+    load_twiddles<H>(tw, t, p.tw);
     float2 v[E];
 
     // GD gradient needs this iteration's global max of |F|^2 (src/algorithms.py:86).
@@ -319,7 +350,7 @@ __global__ void __launch_bounds__((ColCfg<H, CW>::THREADS)) col_kernel(ColParams
     if constexpr (MODE == COL_REAL_INV) {
 #pragma unroll
         for (int m = 0; m < E; ++m) {
-            const float tv = TgtLoad<TT>::load(p.tgt, base + (long long)(t + T * m) * p.W);
+            const float tv = TgtLoad<TT>::load(p.tgt, base + m * kStep);
             v[m] = make_float2(TgtLoad<TT>::amp(tv), 0.0f);
         }
     } else if constexpr (MODE == COL_EXPECTED) {
@@ -327,36 +358,41 @@ __global__ void __launch_bounds__((ColCfg<H, CW>::THREADS)) col_kernel(ColParams
         const int s = min(p.stop_iter[b], p.loops - 1);
         const float2* src = (s & 1) ? p.in_alt : p.in;
 #pragma unroll
-        for (int m = 0; m < E; ++m) v[m] = src[base + (long long)(t + T * m) * p.W];
+        for (int m = 0; m < E; ++m) v[m] = src[base + m * kStep];
     } else {
 #pragma unroll
-        for (int m = 0; m < E; ++m) v[m] = p.in[base + (long long)(t + T * m) * p.W];
+        for (int m = 0; m < E; ++m) v[m] = p.in[base + m * kStep];
+    }
+    // the stop test is issued behind the loads so its latency overlaps them
+    if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_STATS || MODE == COL_GD_GRAD) {
+        if (p.iter > p.stop_iter[b]) return;
     }
 
     if constexpr (MODE == COL_REAL_INV || MODE == COL_FFT_INV) {
-        fft_line<H, true>(v, t, p.tw, lds);
+        fft_line<H, true>(v, t, tw, lds);
 #pragma unroll
-        for (int m = 0; m < E; ++m) p.out[base + (long long)(t + T * m) * p.W] = v[m];
+        for (int m = 0; m < E; ++m) p.out[base + m * kStep] = v[m];
         return;
     } else {
-        fft_line<H, false>(v, t, p.tw, lds);
+        fft_line<H, false>(v, t, tw, lds);
     }
 
     if constexpr (MODE == COL_FFT_FWD) {
 #pragma unroll
-        for (int m = 0; m < E; ++m) p.out[base + (long long)(t + T * m) * p.W] = v[m];
+        for (int m = 0; m < E; ++m) p.out[base + m * kStep] = v[m];
         return;
     } else if constexpr (MODE == COL_EXPECTED) {
+        const long long nat = (long long)b * p.holo + (long long)t * p.W + x;  // row-major output
 #pragma unroll
         for (int m = 0; m < E; ++m)
-            p.e_out[base + (long long)(t + T * m) * p.W] = v[m].x * v[m].x + v[m].y * v[m].y;
+            p.e_out[nat + (long long)m * T * p.W] = v[m].x * v[m].x + v[m].y * v[m].y;
         return;
     } else {
         double mx = 0.0, s2 = 0.0, st = 0.0;
         const float norm = (MODE == COL_GD_GRAD) ? p.norm[b] : 0.0f;
 #pragma unroll
         for (int m = 0; m < E; ++m) {
-            const float tv = TgtLoad<TT>::load(p.tgt, base + (long long)(t + T * m) * p.W);
+            const float tv = TgtLoad<TT>::load(p.tgt, base + m * kStep);
             const float e = v[m].x * v[m].x + v[m].y * v[m].y;
             if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_STATS) {
                 const double ed = (double)e;
@@ -384,9 +420,9 @@ __global__ void __launch_bounds__((ColCfg<H, CW>::THREADS)) col_kernel(ColParams
             }
         }
         if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD) {
-            fft_line<H, true>(v, t, p.tw, lds);
+            fft_line<H, true>(v, t, tw, lds);
 #pragma unroll
-            for (int m = 0; m < E; ++m) p.out[base + (long long)(t + T * m) * p.W] = v[m];
+            for (int m = 0; m < E; ++m) p.out[base + m * kStep] = v[m];
         }
     }
 }
@@ -453,10 +489,32 @@ __global__ void __launch_bounds__(256) stats_finalize_kernel(StatsParams p) {
     }
 }
 
-// hologram = np.angle(input) of the GD field (src/algorithms.py:111).
-__global__ void __launch_bounds__(256) field_phase_kernel(const float2* field, float* phase, long long n) {
-    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
-        phase[i] = atan2f(field[i].y, field[i].x);
+// hologram = np.angle(input) of the GD field (src/algorithms.py:111); the
+// field is in the blocked layout, the phase row-major.
+__global__ void __launch_bounds__(256) field_phase_kernel(const float2* field, float* phase, long long n, int H,
+                                                          int W) {
+    const long long holo = (long long)H * W;
+    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+        const long long b = i / holo, r = i - b * holo;
+        const int y = (int)(r / W), x = (int)(r - (long long)y * W);
+        const float2 f = field[b * holo + blk_index(y, x, H)];
+        phase[i] = atan2f(f.y, f.x);
+    }
+}
+
+// row-major <-> blocked layout (uploads, the FFT test entry)
+template <typename V, bool TO_BLOCKED>
+__global__ void __launch_bounds__(256) relayout_kernel(const V* in, V* out, long long n, int H, int W) {
+    const long long holo = (long long)H * W;
+    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+        const long long b = i / holo, r = i - b * holo;
+        const int y = (int)(r / W), x = (int)(r - (long long)y * W);
+        const long long j = b * holo + blk_index(y, x, H);
+        if (TO_BLOCKED)
+            out[j] = in[i];
+        else
+            out[i] = in[j];
+    }
 }
 
 #endif  // SLM_DEFINE_SMALL_KERNELS

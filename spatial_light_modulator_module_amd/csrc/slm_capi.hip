@@ -117,23 +117,50 @@ __global__ void fill_int_kernel(int* p, int n, int v) {
 
 // max(T) and sum(T^2) per hologram in double (np.amax(demanded_output),
 // src/algorithms.py:23; sum(T^2) is the constant term of the error expansion).
+// Stage 1: kTsBlocks workgroups per hologram reduce contiguous chunks.
+constexpr int kTsBlocks = 64;
 template <typename TT>
-__global__ void __launch_bounds__(256) target_stats_kernel(const TT* tgt, long long holo, double* norm,
-                                                            float* normf, double* sum_t2) {
-    const int b = blockIdx.x;
+__global__ void __launch_bounds__(256) target_stats_partial_kernel(const TT* tgt, long long holo, double* part) {
+    const int b = blockIdx.y;
+    const long long chunk = (holo + kTsBlocks - 1) / kTsBlocks;
+    const long long lo = (long long)blockIdx.x * chunk, hi = min(holo, lo + chunk);
     const TT* p = tgt + (long long)b * holo;
     double mx = 0.0, s2 = 0.0, d = 0.0;
-    for (long long i = threadIdx.x; i < holo; i += 256) {
+    for (long long i = lo + threadIdx.x; i < hi; i += 256) {
         const double v = (double)p[i];
         mx = fmax(mx, v);
         s2 += v * v;
     }
     block_reduce_stats<256>(mx, s2, d);
     if (threadIdx.x == 0) {
+        double* o = part + ((long long)b * kTsBlocks + blockIdx.x) * 2;
+        o[0] = mx;
+        o[1] = s2;
+    }
+}
+__global__ void __launch_bounds__(64) target_stats_final_kernel(const double* part, double* norm, float* normf,
+                                                                double* sum_t2) {
+    const int b = blockIdx.x;
+    double mx = part[((long long)b * kTsBlocks + threadIdx.x) * 2];
+    double s2 = part[((long long)b * kTsBlocks + threadIdx.x) * 2 + 1];
+    double d = 0.0;
+    block_reduce_stats<64>(mx, s2, d);
+    if (threadIdx.x == 0) {
         norm[b] = mx;
         normf[b] = (float)mx;
         sum_t2[b] = s2;
     }
+}
+
+template <typename V>
+int relayout(const V* in, V* out, long long n, int H, int W, bool to_blocked, hipStream_t st) {
+    const int grid = (int)std::min<long long>(8192, (n + 255) / 256);
+    if (to_blocked)
+        hipLaunchKernelGGL((relayout_kernel<V, true>), dim3(grid), dim3(256), 0, st, in, out, n, H, W);
+    else
+        hipLaunchKernelGGL((relayout_kernel<V, false>), dim3(grid), dim3(256), 0, st, in, out, n, H, W);
+    HIP_TRY(hipGetLastError());
+    return 0;
 }
 
 }  // namespace
@@ -158,6 +185,7 @@ struct slm_plan {
     double* norm = nullptr;
     float* normf = nullptr;
     double* sum_t2 = nullptr;
+    double* ts_part = nullptr;
     float* lr = nullptr;
     float* gather_buf = nullptr;
     long long gather_elems = 0;
@@ -171,19 +199,18 @@ struct slm_plan {
 
 namespace {
 
+// Column tile width. With the blocked state layout a 4-column panel is one
+// contiguous run, so the narrowest tile already moves whole lines and keeps
+// the most workgroups (and LDS headroom) per CU; SLM_COL_CW overrides.
 int pick_cw(int H, int W, int B) {
+    (void)B;
     if (const char* s = std::getenv("SLM_COL_CW")) {
         const int cw = std::atoi(s);
         if (col_fn(H, cw, COL_GS_MAIN, TGT_F32) && W % cw == 0) return cw;
     }
-    const int cands[3] = {16, 8, 4};
-    int best = 0;
-    for (int cw : cands) {
-        if (W % cw || !col_fn(H, cw, COL_GS_MAIN, TGT_F32)) continue;
-        if ((long long)(W / cw) * B >= 1024) return cw;
-        best = cw;  // keeps the smallest valid tile: most workgroups
-    }
-    return best;
+    for (int cw : {4, 8, 16})
+        if (W % cw == 0 && col_fn(H, cw, COL_GS_MAIN, TGT_F32)) return cw;
+    return 0;
 }
 
 int begin_launch(slm_plan* p, int cls) {
@@ -215,6 +242,7 @@ RowParams row_params(slm_plan* p) {
     r.lr = p->lr;
     r.stop_iter = p->stop;
     r.W = p->W;
+    r.H = p->H;
     r.holo = p->holo;
     r.inv_s = (float)(1.0 / (double)p->holo);
     r.tw = p->tw_row;
@@ -363,7 +391,7 @@ int enqueue_gd(slm_plan* p, int loops, double tol, int checked, float wa) {
         const long long n = (long long)p->B * p->holo;
         const int grid = (int)std::min<long long>(4096, (n + 255) / 256);
         hipLaunchKernelGGL(field_phase_kernel, dim3(grid), dim3(256), 0, p->stream, (const float2*)p->field,
-                           p->phase_out, n);
+                           p->phase_out, n, p->H, p->W);
         HIP_TRY(hipGetLastError());
         RC(end_launch(p));
     }
@@ -403,7 +431,7 @@ void free_plan(slm_plan* p) {
     for (void* ptr : {(void*)p->xa, (void*)p->xb, (void*)p->y, (void*)p->field, p->tgt, (void*)p->ain,
                       (void*)p->phase_in, (void*)p->phase_out, (void*)p->e_out, (void*)p->partials,
                       (void*)p->stats, (void*)p->stop, (void*)p->norm, (void*)p->normf, (void*)p->sum_t2,
-                      (void*)p->lr, (void*)p->gather_buf})
+                      (void*)p->ts_part, (void*)p->lr, (void*)p->gather_buf})
         if (ptr) (void)hipFree(ptr);
     for (auto& e : p->ev_pool) {
         (void)hipEventDestroy(e.first);
@@ -514,6 +542,7 @@ int slm_plan_create(int algo, int batch, int height, int width, int tgt_type, in
     RC(alloc((void**)&p->norm, (size_t)batch * sizeof(double)));
     RC(alloc((void**)&p->normf, (size_t)batch * sizeof(float)));
     RC(alloc((void**)&p->sum_t2, (size_t)batch * sizeof(double)));
+    RC(alloc((void**)&p->ts_part, (size_t)batch * kTsBlocks * 2 * sizeof(double)));
     *out = p;
     return 0;
 }
@@ -526,14 +555,21 @@ int slm_plan_destroy(slm_plan* plan) {
 int slm_plan_set_target(slm_plan* p, const void* tgt) {
     if (!p || !tgt) return fail(SLM_ERR_ARG, "null argument");
     HIP_TRY(hipSetDevice(p->device));
+    const long long n = (long long)p->B * p->holo;
     const size_t tb = p->tt == SLM_TGT_U8 ? 1 : 4;
-    HIP_TRY(hipMemcpyAsync(p->tgt, tgt, (size_t)p->B * p->holo * tb, hipMemcpyHostToDevice, p->stream));
-    if (p->tt == SLM_TGT_U8)
-        hipLaunchKernelGGL(target_stats_kernel<uint8_t>, dim3(p->B), dim3(256), 0, p->stream,
-                           (const uint8_t*)p->tgt, p->holo, p->norm, p->normf, p->sum_t2);
-    else
-        hipLaunchKernelGGL(target_stats_kernel<float>, dim3(p->B), dim3(256), 0, p->stream, (const float*)p->tgt,
-                           p->holo, p->norm, p->normf, p->sum_t2);
+    void* stage = p->e_out;  // n floats >= n target elements of either type
+    HIP_TRY(hipMemcpyAsync(stage, tgt, (size_t)n * tb, hipMemcpyHostToDevice, p->stream));
+    if (p->tt == SLM_TGT_U8) {
+        hipLaunchKernelGGL(target_stats_partial_kernel<uint8_t>, dim3(kTsBlocks, p->B), dim3(256), 0, p->stream,
+                           (const uint8_t*)stage, p->holo, p->ts_part);
+        RC(relayout((const uint8_t*)stage, (uint8_t*)p->tgt, n, p->H, p->W, true, p->stream));
+    } else {
+        hipLaunchKernelGGL(target_stats_partial_kernel<float>, dim3(kTsBlocks, p->B), dim3(256), 0, p->stream,
+                           (const float*)stage, p->holo, p->ts_part);
+        RC(relayout((const float*)stage, (float*)p->tgt, n, p->H, p->W, true, p->stream));
+    }
+    hipLaunchKernelGGL(target_stats_final_kernel, dim3(p->B), dim3(kTsBlocks), 0, p->stream, p->ts_part, p->norm,
+                       p->normf, p->sum_t2);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(p->stream));
     p->target_set = true;
@@ -571,7 +607,10 @@ int slm_plan_set_field(slm_plan* p, const float* field) {
         p->field_set = false;
         return 0;
     }
-    HIP_TRY(hipMemcpy(p->field, field, (size_t)p->B * p->holo * sizeof(float2), hipMemcpyHostToDevice));
+    const long long n = (long long)p->B * p->holo;
+    HIP_TRY(hipMemcpyAsync(p->y, field, (size_t)n * sizeof(float2), hipMemcpyHostToDevice, p->stream));
+    RC(relayout((const float2*)p->y, p->field, n, p->H, p->W, true, p->stream));
+    HIP_TRY(hipStreamSynchronize(p->stream));
     p->field_set = true;
     return 0;
 }
@@ -703,10 +742,12 @@ int slm_fft2(const float* in, float* out, int batch, int height, int width, int 
     if (!in || !out) return fail(SLM_ERR_ARG, "null argument");
     slm_plan* p = nullptr;
     RC(slm_plan_create(SLM_ALGO_GS, batch, height, width, SLM_TGT_F32, 0, 1, &p));
-    const size_t bytes = (size_t)batch * p->holo * sizeof(float2);
+    const long long n = (long long)batch * p->holo;
+    const size_t bytes = (size_t)n * sizeof(float2);
     int rc = 0;
-    hipError_t e = hipMemcpy(p->xa, in, bytes, hipMemcpyHostToDevice);
+    hipError_t e = hipMemcpyAsync(p->y, in, bytes, hipMemcpyHostToDevice, p->stream);
     if (e != hipSuccess) rc = fail(SLM_ERR_HIP, "upload failed: %s", hipGetErrorString(e));
+    if (!rc) rc = relayout((const float2*)p->y, p->xa, n, height, width, true, p->stream);
     if (!rc) {
         RowParams rp = row_params(p);
         rp.in = p->xa;
@@ -719,9 +760,10 @@ int slm_fft2(const float* in, float* out, int batch, int height, int width, int 
         cp.out = p->xa;
         rc = launch_col(p, inverse ? COL_FFT_INV : COL_FFT_FWD, cp, SLM_KERNEL_OTHER);
     }
+    if (!rc) rc = relayout((const float2*)p->xa, p->y, n, height, width, false, p->stream);
     if (!rc) {
         e = hipStreamSynchronize(p->stream);
-        if (e == hipSuccess) e = hipMemcpy(out, p->xa, bytes, hipMemcpyDeviceToHost);
+        if (e == hipSuccess) e = hipMemcpy(out, p->y, bytes, hipMemcpyDeviceToHost);
         if (e != hipSuccess) rc = fail(SLM_ERR_HIP, "fft2 failed: %s", hipGetErrorString(e));
     }
     free_plan(p);

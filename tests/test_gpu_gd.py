@@ -33,6 +33,7 @@ def test_gd_100_parity_vs_reference(gpu, golden_dir):
     g = golden(golden_dir, "g4_gd_f32_256.npz")
     holo, out, err = gradient_descent(g["target"], gd_args(max_loops=100))
     rms = orc.phase_rms(holo, g["phi100"])
+    print(f"[parity] GD 100 loops: phase rms {rms:.3e}")
     assert rms < 1e-5, f"phase rms {rms:.3e}"
     np.testing.assert_allclose(err, g["err100"], rtol=1e-4)
     np.testing.assert_allclose(out, g["output100"], rtol=2e-3, atol=0.05)
@@ -46,6 +47,7 @@ def test_gd_500_error_curve_vs_reference(gpu, golden_dir):
     holo, _, err = gradient_descent(g["target"], gd_args(max_loops=500))
     np.testing.assert_allclose(err, g["err500"], rtol=1e-3)
     rms = orc.phase_rms(holo, g["phi500"])
+    print(f"[parity] GD 500 loops: phase rms {rms:.3e}")
     assert rms < 2e-4, f"phase rms {rms:.3e}"  # float32 drift floor ~5e-5
 
 

@@ -36,6 +36,7 @@ def test_gs_warm_start_parity_vs_reference(gpu, golden_dir, name):
     g = golden(golden_dir, name)
     phase, e, errs, norm, emax = alg.run_gs(g["target"][None], 200, initial_phase=g["phi30"][None])
     rms = orc.phase_rms(phase[0], g["phi230"])
+    print(f"[parity] {name} warm-start 200 loops: phase rms {rms:.3e}")
     assert rms < PHASE_RMS_TOL, f"phase rms {rms:.3e}"
     err = np.array(errs[0])
     np.testing.assert_allclose(err, g["err230"][30:], rtol=1e-4)
