@@ -38,6 +38,10 @@ extern "C" {
 #define SLM_TGT_U8 0  /* uint8 target; amplitude = float16(sqrt(T)) as numpy does */
 #define SLM_TGT_F32 1 /* float32 target; amplitude = sqrtf(T) */
 
+/* arithmetic precision of the transforms (state is complex64 in HBM either way) */
+#define SLM_PRECISION_F32 0 /* float32 butterflies and twiddles */
+#define SLM_PRECISION_F64 1 /* float64 butterflies and twiddles (default; $SLM_PRECISION=f32 overrides) */
+
 /* kernel classes for timing / roofline queries */
 #define SLM_KERNEL_COL_MAIN 0 /* GS column pass, or GD gradient column pass */
 #define SLM_KERNEL_ROW_MAIN 1 /* GS / GD fused row pass */
@@ -69,6 +73,8 @@ int slm_plan_destroy(slm_plan* plan);
 /* targets [batch][height][width] of tgt_type; norm = max(T) and sum(T^2) are
  * reduced on the device */
 int slm_plan_set_target(slm_plan* plan, const void* tgt);
+int slm_plan_set_precision(slm_plan* plan, int precision);       /* SLM_PRECISION_* */
+int slm_plan_get_precision(slm_plan* plan);
 int slm_plan_set_ain(slm_plan* plan, const float* ain);           /* [height][width] sqrt(incoming intensity) */
 int slm_plan_set_phase(slm_plan* plan, const float* phase);       /* GS warm start [batch][h][w]; NULL = cold */
 int slm_plan_set_field(slm_plan* plan, const float* field_re_im); /* GD initial x [batch][h][w][2]; NULL = fourier */

@@ -17,6 +17,8 @@ ALGO_GS = 0
 ALGO_GD = 1
 TGT_U8 = 0
 TGT_F32 = 1
+PRECISION_F32 = 0
+PRECISION_F64 = 1
 
 KERNEL_COL_MAIN = 0
 KERNEL_ROW_MAIN = 1
@@ -48,6 +50,8 @@ _SIGNATURES = [
     ("slm_plan_create", _c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _P(_vp)]),
     ("slm_plan_destroy", _c_int, [_vp]),
     ("slm_plan_set_target", _c_int, [_vp, _vp]),
+    ("slm_plan_set_precision", _c_int, [_vp, _c_int]),
+    ("slm_plan_get_precision", _c_int, [_vp]),
     ("slm_plan_set_ain", _c_int, [_vp, _vp]),
     ("slm_plan_set_phase", _c_int, [_vp, _vp]),
     ("slm_plan_set_field", _c_int, [_vp, _vp]),
@@ -165,6 +169,13 @@ class Plan:
         dt = np.uint8 if self.tgt_type == TGT_U8 else np.float32
         a = np.ascontiguousarray(tgt, dtype=dt).reshape(self.shape)
         check(self._lib.slm_plan_set_target(self.handle, ptr(a)), "slm_plan_set_target")
+
+    @property
+    def precision(self) -> int:
+        return int(self._lib.slm_plan_get_precision(self.handle))
+
+    def set_precision(self, precision: int) -> None:
+        check(self._lib.slm_plan_set_precision(self.handle, int(precision)), "slm_plan_set_precision")
 
     def set_ain(self, ain: np.ndarray) -> None:
         a = np.ascontiguousarray(ain, dtype=np.float32).reshape(self.height, self.width)

@@ -10,8 +10,8 @@ using RowFn = void (*)(RowParams);
 using ColFn = void (*)(ColParams);
 
 #define SLM_DECLARE_LENGTH(N)                    \
-    RowFn row_fn_##N(int mode);                  \
-    ColFn col_fn_##N(int cw, int mode, int tt);  \
+    RowFn row_fn_##N(int mode, int prec);                  \
+    ColFn col_fn_##N(int cw, int mode, int tt, int prec);  \
     int row_threads_##N();                       \
     int row_rpw_##N();                           \
     int col_threads_##N(int cw);
@@ -27,15 +27,15 @@ SLM_DECLARE_LENGTH(4096)
 
 #define SLM_FOR_EACH_LENGTH(X) X(64) X(128) X(256) X(512) X(768) X(1024) X(2048) X(4096)
 
-inline RowFn row_fn(int n, int mode) {
+inline RowFn row_fn(int n, int mode, int prec) {
 #define SLM_CASE(N) \
-    case N: return row_fn_##N(mode);
+    case N: return row_fn_##N(mode, prec);
     switch (n) { SLM_FOR_EACH_LENGTH(SLM_CASE) default: return nullptr; }
 #undef SLM_CASE
 }
-inline ColFn col_fn(int n, int cw, int mode, int tt) {
+inline ColFn col_fn(int n, int cw, int mode, int tt, int prec) {
 #define SLM_CASE(N) \
-    case N: return col_fn_##N(cw, mode, tt);
+    case N: return col_fn_##N(cw, mode, tt, prec);
     switch (n) { SLM_FOR_EACH_LENGTH(SLM_CASE) default: return nullptr; }
 #undef SLM_CASE
 }

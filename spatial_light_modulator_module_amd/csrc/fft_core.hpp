@@ -11,6 +11,13 @@
 //     round trip (the fused GS/GD iteration relies on this).
 // Forward = exp(-2 pi i nk/N), unscaled (scipy.fft.fft2, src/algorithms.py:31);
 // inverse = exp(+2 pi i nk/N), unscaled (callers apply 1/N where needed).
+//
+// Precision. The arithmetic type C is float2 or double2. HBM state and LDS
+// exchanges are always complex64; with C = double2 the butterflies and the
+// twiddles (table computed in double on the host) run in float64, so a
+// transform rounds only where it stores. Simulated on the reference's GS
+// warm-start protocol (Precision) this cuts the float32 phase drift
+// ~10x; the cost is FP64 VALU work and registers.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <type_traits>
@@ -80,79 +87,97 @@ constexpr double cos48(int q) {
 constexpr double sin48(int q) { return cos48(q - 12); }
 
 // ------------------------------------------------------------------------
-// complex helpers (float2 = interleaved complex64, the HBM layout)
+// complex helpers; C = float2 or double2
 // ------------------------------------------------------------------------
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+template <class C>
+using Scalar = std::remove_reference_t<decltype(C{}.x)>;
+
+template <class C>
+__device__ __forceinline__ C mk(Scalar<C> x, Scalar<C> y) {
+    C r;
+    r.x = x;
+    r.y = y;
+    return r;
 }
+template <class C>
+__device__ __forceinline__ C cadd(C a, C b) { return mk<C>(a.x + b.x, a.y + b.y); }
+template <class C>
+__device__ __forceinline__ C csub(C a, C b) { return mk<C>(a.x - b.x, a.y - b.y); }
+template <class C>
+__device__ __forceinline__ C cmul(C a, C b) { return mk<C>(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); }
 // a * conj(b)
-__device__ __forceinline__ float2 cmulc(float2 a, float2 b) {
-    return make_float2(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
-}
+template <class C>
+__device__ __forceinline__ C cmulc(C a, C b) { return mk<C>(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y); }
+
+// complex64 storage <-> compute type
+template <class C>
+__device__ __forceinline__ C from_c64(float2 v) { return mk<C>((Scalar<C>)v.x, (Scalar<C>)v.y); }
+template <class C>
+__device__ __forceinline__ float2 to_c64(C v) { return make_float2((float)v.x, (float)v.y); }
 
 // Multiply by the constant twiddle w_R^K (forward: exp(-2 pi i K/R)).
-template <int K, int R, bool INV>
-__device__ __forceinline__ float2 twc(float2 a) {
+template <int K, int R, bool INV, class C>
+__device__ __forceinline__ C twc(C a) {
+    using S = Scalar<C>;
     constexpr int q = ((48 / R) * K) % 48;
     if constexpr (q == 0) {
         return a;
     } else if constexpr (q == 24) {
-        return make_float2(-a.x, -a.y);
+        return mk<C>(-a.x, -a.y);
     } else if constexpr (q == 12) {  // forward: * (-i)
-        return INV ? make_float2(-a.y, a.x) : make_float2(a.y, -a.x);
+        return INV ? mk<C>(-a.y, a.x) : mk<C>(a.y, -a.x);
     } else if constexpr (q == 36) {  // forward: * (+i)
-        return INV ? make_float2(a.y, -a.x) : make_float2(-a.y, a.x);
+        return INV ? mk<C>(a.y, -a.x) : mk<C>(-a.y, a.x);
     } else {
-        constexpr float c = (float)cos48(q);
-        constexpr float s = (float)(INV ? sin48(q) : -sin48(q));
-        return make_float2(a.x * c - a.y * s, a.x * s + a.y * c);
+        constexpr S c = (S)cos48(q);
+        constexpr S s = (S)(INV ? sin48(q) : -sin48(q));
+        return mk<C>(a.x * c - a.y * s, a.x * s + a.y * c);
     }
 }
 
 // ------------------------------------------------------------------------
 // in-register DFTs, natural order in and out
 // ------------------------------------------------------------------------
-template <int R, bool INV>
+template <int R, bool INV, class C>
 struct Dft;
 
-template <bool INV>
-struct Dft<1, INV> {
-    __device__ __forceinline__ static void run(float2*) {}
+template <bool INV, class C>
+struct Dft<1, INV, C> {
+    __device__ __forceinline__ static void run(C*) {}
 };
 
-template <bool INV>
-struct Dft<2, INV> {
-    __device__ __forceinline__ static void run(float2* v) {
-        const float2 a = v[0], b = v[1];
+template <bool INV, class C>
+struct Dft<2, INV, C> {
+    __device__ __forceinline__ static void run(C* v) {
+        const C a = v[0], b = v[1];
         v[0] = cadd(a, b);
         v[1] = csub(a, b);
     }
 };
 
-template <bool INV>
-struct Dft<3, INV> {
-    __device__ __forceinline__ static void run(float2* v) {
-        constexpr float h = 0.86602540378443865f;  // sqrt(3)/2
-        const float2 s = cadd(v[1], v[2]);
-        const float2 d = csub(v[1], v[2]);
-        const float2 t = make_float2(v[0].x - 0.5f * s.x, v[0].y - 0.5f * s.y);
+template <bool INV, class C>
+struct Dft<3, INV, C> {
+    __device__ __forceinline__ static void run(C* v) {
+        using S = Scalar<C>;
+        constexpr S h = (S)0.86602540378443865;  // sqrt(3)/2
+        const C s = cadd(v[1], v[2]);
+        const C d = csub(v[1], v[2]);
+        const C t = mk<C>(v[0].x - (S)0.5 * s.x, v[0].y - (S)0.5 * s.y);
         // forward: (-i) * h * d ; inverse: (+i) * h * d
-        const float2 m = INV ? make_float2(-h * d.y, h * d.x) : make_float2(h * d.y, -h * d.x);
+        const C m = INV ? mk<C>(-h * d.y, h * d.x) : mk<C>(h * d.y, -h * d.x);
         v[0] = cadd(v[0], s);
         v[1] = cadd(t, m);
         v[2] = csub(t, m);
     }
 };
 
-template <bool INV>
-struct Dft<4, INV> {
-    __device__ __forceinline__ static void run(float2* v) {
-        const float2 a = cadd(v[0], v[2]);
-        const float2 b = csub(v[0], v[2]);
-        const float2 c = cadd(v[1], v[3]);
-        const float2 d = twc<1, 4, INV>(csub(v[1], v[3]));
+template <bool INV, class C>
+struct Dft<4, INV, C> {
+    __device__ __forceinline__ static void run(C* v) {
+        const C a = cadd(v[0], v[2]);
+        const C b = csub(v[0], v[2]);
+        const C c = cadd(v[1], v[3]);
+        const C d = twc<1, 4, INV>(csub(v[1], v[3]));
         v[0] = cadd(a, c);
         v[2] = csub(a, c);
         v[1] = cadd(b, d);
@@ -161,18 +186,18 @@ struct Dft<4, INV> {
 };
 
 // Cooley-Tukey split R = R1 * R2: n = R2 n1 + n2, k = k1 + R1 k2.
-template <int R1, int R2, bool INV>
-__device__ __forceinline__ void dft_split(float2* v) {
+template <int R1, int R2, bool INV, class C>
+__device__ __forceinline__ void dft_split(C* v) {
     constexpr int R = R1 * R2;
-    float2 z[R];
+    C z[R];
     static_for<R2>([&](auto n2c) {
         constexpr int n2 = decltype(n2c)::value;
-        float2 col[R1];
+        C col[R1];
         static_for<R1>([&](auto n1c) {
             constexpr int n1 = decltype(n1c)::value;
             col[n1] = v[R2 * n1 + n2];
         });
-        Dft<R1, INV>::run(col);
+        Dft<R1, INV, C>::run(col);
         static_for<R1>([&](auto k1c) {
             constexpr int k1 = decltype(k1c)::value;
             z[n2 * R1 + k1] = twc<n2 * k1, R, INV>(col[k1]);
@@ -180,12 +205,12 @@ __device__ __forceinline__ void dft_split(float2* v) {
     });
     static_for<R1>([&](auto k1c) {
         constexpr int k1 = decltype(k1c)::value;
-        float2 row[R2];
+        C row[R2];
         static_for<R2>([&](auto n2c) {
             constexpr int n2 = decltype(n2c)::value;
             row[n2] = z[n2 * R1 + k1];
         });
-        Dft<R2, INV>::run(row);
+        Dft<R2, INV, C>::run(row);
         static_for<R2>([&](auto k2c) {
             constexpr int k2 = decltype(k2c)::value;
             v[k1 + R1 * k2] = row[k2];
@@ -193,23 +218,23 @@ __device__ __forceinline__ void dft_split(float2* v) {
     });
 }
 
-template <bool INV>
-struct Dft<8, INV> {
-    __device__ __forceinline__ static void run(float2* v) { dft_split<2, 4, INV>(v); }
+template <bool INV, class C>
+struct Dft<8, INV, C> {
+    __device__ __forceinline__ static void run(C* v) { dft_split<2, 4, INV, C>(v); }
 };
-template <bool INV>
-struct Dft<12, INV> {
-    __device__ __forceinline__ static void run(float2* v) { dft_split<4, 3, INV>(v); }
+template <bool INV, class C>
+struct Dft<12, INV, C> {
+    __device__ __forceinline__ static void run(C* v) { dft_split<4, 3, INV, C>(v); }
 };
-template <bool INV>
-struct Dft<16, INV> {
-    __device__ __forceinline__ static void run(float2* v) { dft_split<4, 4, INV>(v); }
+template <bool INV, class C>
+struct Dft<16, INV, C> {
+    __device__ __forceinline__ static void run(C* v) { dft_split<4, 4, INV, C>(v); }
 };
 
 // ------------------------------------------------------------------------
-// LDS views. A pass writes output element o and reads element t + T m of the
-// line; padding one slot per 16 keeps the strided first-pass writes off a
-// single bank.
+// LDS views (complex64). A pass writes output element o and reads element
+// t + T m of the line; padding one slot per 16 keeps the strided first-pass
+// writes off a single bank.
 // ------------------------------------------------------------------------
 struct LdsLine {  // one transform line per thread group (row kernels)
     float2* base;
@@ -227,9 +252,10 @@ struct LdsTile {  // CW interleaved columns (column kernels): [o][c]
 
 // ------------------------------------------------------------------------
 // Per-thread twiddles. Which twiddles a thread needs depends only on its
-// transform-thread index t, so they are loaded once per kernel (one global
-// load each, table computed in double on the host) and shared by every
-// transform the thread runs (inverse and forward use conjugates).
+// transform-thread index t, so they can be loaded once per kernel (one global
+// load each; table computed in double on the host, stored as the compute
+// type) and shared by every transform the thread runs (inverse and forward
+// use conjugates).
 // ------------------------------------------------------------------------
 template <int N, int Ns, int... Rs>
 struct TwCountImpl;
@@ -249,28 +275,28 @@ struct TwCountOf<N, IntList<Rs...>> {
 };
 
 // CACHED: every twiddle of the thread in registers (one load each per kernel).
-// !CACHED: read from the (L1/L2-resident) table where used — for 1024-thread
-// workgroups whose 128-VGPR budget cannot hold the cache.
-template <int N, bool CACHED = true>
+// !CACHED: read from the (L1/L2-resident) table where used — when the
+// register budget of the workgroup cannot hold the cache.
+template <int N, class C, bool CACHED>
 struct Twiddles {
     static constexpr int COUNT = TwCountOf<N, RadicesOf<N>>::value > 0 ? TwCountOf<N, RadicesOf<N>>::value : 1;
-    float2 w[COUNT];
+    C w[COUNT];
     template <int TwOff, int RegOff, int R, int Ns>
-    __device__ __forceinline__ float2 get(int k, int r, int j) const {
+    __device__ __forceinline__ C get(int k, int r, int) const {
         return w[RegOff + k * (R - 1) + r - 1];
     }
 };
-template <int N>
-struct Twiddles<N, false> {
-    const float2* __restrict__ table;
+template <int N, class C>
+struct Twiddles<N, C, false> {
+    const C* __restrict__ table;
     template <int TwOff, int RegOff, int R, int Ns>
-    __device__ __forceinline__ float2 get(int k, int r, int j) const {
+    __device__ __forceinline__ C get(int, int r, int j) const {
         return table[TwOff + (r - 1) * Ns + j];
     }
 };
 
-template <int N, int E, int Ns, int TwOff, int RegOff, int R, int... Rest>
-__device__ __forceinline__ void load_twiddles_pass(Twiddles<N, true>& tw, int t, const float2* __restrict__ table) {
+template <int N, class C, int E, int Ns, int TwOff, int RegOff, int R, int... Rest>
+__device__ __forceinline__ void load_twiddles_pass(Twiddles<N, C, true>& tw, int t, const C* __restrict__ table) {
     constexpr int T = N / E;
     constexpr int NB = E / R;
     if constexpr (Ns > 1) {
@@ -286,29 +312,28 @@ __device__ __forceinline__ void load_twiddles_pass(Twiddles<N, true>& tw, int t,
     if constexpr (sizeof...(Rest) > 0) {
         constexpr int kNextOff = TwOff + (Ns > 1 ? (R - 1) * Ns : 0);
         constexpr int kNextReg = RegOff + (Ns > 1 ? NB * (R - 1) : 0);
-        load_twiddles_pass<N, E, Ns * R, kNextOff, kNextReg, Rest...>(tw, t, table);
+        load_twiddles_pass<N, C, E, Ns * R, kNextOff, kNextReg, Rest...>(tw, t, table);
     }
 }
-template <int N, int... Rs>
-__device__ __forceinline__ void load_twiddles_impl(Twiddles<N, true>& tw, int t, const float2* table,
-                                                   IntList<Rs...>) {
-    load_twiddles_pass<N, PlanOf<N>::E, 1, 0, 0, Rs...>(tw, t, table);
+template <int N, class C, int... Rs>
+__device__ __forceinline__ void load_twiddles_impl(Twiddles<N, C, true>& tw, int t, const C* table, IntList<Rs...>) {
+    load_twiddles_pass<N, C, PlanOf<N>::E, 1, 0, 0, Rs...>(tw, t, table);
 }
-template <int N>
-__device__ __forceinline__ void load_twiddles(Twiddles<N, true>& tw, int t, const float2* __restrict__ table) {
-    load_twiddles_impl<N>(tw, t, table, RadicesOf<N>{});
+template <int N, class C>
+__device__ __forceinline__ void load_twiddles(Twiddles<N, C, true>& tw, int t, const void* table) {
+    load_twiddles_impl<N, C>(tw, t, static_cast<const C*>(table), RadicesOf<N>{});
 }
-template <int N>
-__device__ __forceinline__ void load_twiddles(Twiddles<N, false>& tw, int, const float2* __restrict__ table) {
-    tw.table = table;
+template <int N, class C>
+__device__ __forceinline__ void load_twiddles(Twiddles<N, C, false>& tw, int, const void* table) {
+    tw.table = static_cast<const C*>(table);
 }
 
 // ------------------------------------------------------------------------
 // Stockham driver. v[m] holds element t + T m on entry and the transform's
 // element t + T m on exit.
 // ------------------------------------------------------------------------
-template <int N, int E, bool INV, int Ns, int TwOff, int RegOff, class Lds, class Tw, int R, int... Rest>
-__device__ __forceinline__ void stockham_pass(float2 (&v)[E], int t, const Tw& tw, const Lds& lds) {
+template <int N, int E, bool INV, int Ns, int TwOff, int RegOff, class C, class Lds, class Tw, int R, int... Rest>
+__device__ __forceinline__ void stockham_pass(C (&v)[E], int t, const Tw& tw, const Lds& lds) {
     constexpr int T = N / E;
     constexpr int NB = E / R;
     static_assert(E % R == 0, "radix must divide elements per thread");
@@ -316,7 +341,7 @@ __device__ __forceinline__ void stockham_pass(float2 (&v)[E], int t, const Tw& t
         constexpr int k = decltype(kc)::value;
         const int b = t + k * T;
         const int j = (Ns == 1) ? 0 : (b % Ns);
-        float2 u[R];
+        C u[R];
         static_for<R>([&](auto rc) {
             constexpr int r = decltype(rc)::value;
             u[r] = v[k + r * NB];
@@ -324,11 +349,11 @@ __device__ __forceinline__ void stockham_pass(float2 (&v)[E], int t, const Tw& t
         if constexpr (Ns > 1) {
             static_for<R - 1>([&](auto rc) {
                 constexpr int r = decltype(rc)::value + 1;
-                const float2 w = tw.template get<TwOff, RegOff, R, Ns>(k, r, j);
+                const C w = tw.template get<TwOff, RegOff, R, Ns>(k, r, j);
                 u[r] = INV ? cmulc(u[r], w) : cmul(u[r], w);
             });
         }
-        Dft<R, INV>::run(u);
+        Dft<R, INV, C>::run(u);
         if constexpr (sizeof...(Rest) == 0) {
             // last pass: Ns * R == N, so b < Ns and output r lands in slot k + r NB
             static_for<R>([&](auto rc) {
@@ -339,7 +364,7 @@ __device__ __forceinline__ void stockham_pass(float2 (&v)[E], int t, const Tw& t
             const int o = (b / Ns) * Ns * R + j;
             static_for<R>([&](auto rc) {
                 constexpr int r = decltype(rc)::value;
-                lds.store(o + r * Ns, u[r]);
+                lds.store(o + r * Ns, to_c64(u[r]));
             });
         }
     });
@@ -347,26 +372,26 @@ __device__ __forceinline__ void stockham_pass(float2 (&v)[E], int t, const Tw& t
         __syncthreads();
         static_for<E>([&](auto mc) {
             constexpr int m = decltype(mc)::value;
-            v[m] = lds.load(t + m * T);
+            v[m] = from_c64<C>(lds.load(t + m * T));
         });
         __syncthreads();
         constexpr int kNextReg = RegOff + (Ns > 1 ? NB * (R - 1) : 0);
         constexpr int kNextOff = TwOff + (Ns > 1 ? (R - 1) * Ns : 0);
-        stockham_pass<N, E, INV, Ns * R, kNextOff, kNextReg, Lds, Tw, Rest...>(v, t, tw, lds);
+        stockham_pass<N, E, INV, Ns * R, kNextOff, kNextReg, C, Lds, Tw, Rest...>(v, t, tw, lds);
     }
 }
 
-template <int N, bool INV, class Lds, class Tw, int... Rs>
-__device__ __forceinline__ void fft_line_impl(float2 (&v)[PlanOf<N>::E], int t, const Tw& tw, const Lds& lds,
+template <int N, bool INV, class C, class Lds, class Tw, int... Rs>
+__device__ __forceinline__ void fft_line_impl(C (&v)[PlanOf<N>::E], int t, const Tw& tw, const Lds& lds,
                                               IntList<Rs...>) {
-    stockham_pass<N, PlanOf<N>::E, INV, 1, 0, 0, Lds, Tw, Rs...>(v, t, tw, lds);
+    stockham_pass<N, PlanOf<N>::E, INV, 1, 0, 0, C, Lds, Tw, Rs...>(v, t, tw, lds);
 }
 
 // Transform one line held in the slot layout. Every thread of the workgroup
 // must call this (it contains workgroup barriers).
-template <int N, bool INV, class Lds, class Tw>
-__device__ __forceinline__ void fft_line(float2 (&v)[PlanOf<N>::E], int t, const Tw& tw, const Lds& lds) {
-    fft_line_impl<N, INV>(v, t, tw, lds, RadicesOf<N>{});
+template <int N, bool INV, class C, class Lds, class Tw>
+__device__ __forceinline__ void fft_line(C (&v)[PlanOf<N>::E], int t, const Tw& tw, const Lds& lds) {
+    fft_line_impl<N, INV, C>(v, t, tw, lds, RadicesOf<N>{});
 }
 
 }  // namespace slm

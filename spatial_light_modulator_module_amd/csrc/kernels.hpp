@@ -42,7 +42,7 @@ struct RowParams {
     int H;                   // rows per hologram (column stride of the blocked layout)
     long long holo;          // elements per hologram (H * W)
     float inv_s;             // 1 / (H * W)
-    const float2* tw;        // twiddle table for length W
+    const void* tw;          // twiddle table for length W (float2 or double2)
 };
 
 struct ColParams {
@@ -61,7 +61,7 @@ struct ColParams {
     int nwg;                 // column workgroups per hologram (W / CW)
     long long holo;          // elements per hologram
     float wa;                // GD white_attention
-    const float2* tw;        // twiddle table for length H
+    const void* tw;          // twiddle table for length H (float2 or double2)
 };
 
 enum RowMode : int {
@@ -93,6 +93,9 @@ enum TgtType : int { TGT_U8 = 0, TGT_F32 = 1, TGT_NUM = 2 };
 
 using RowFn = void (*)(RowParams);
 using ColFn = void (*)(ColParams);
+
+// arithmetic precision of the transforms: 0 = float32, 1 = float64 (storage is complex64 in both)
+enum Precision : int { PREC_F32 = 0, PREC_F64 = 1, PREC_NUM = 2 };
 
 // ------------------------------------------------------------------------
 // geometry
@@ -133,19 +136,36 @@ __host__ __device__ __forceinline__ long long blk_index(long long y, int x, int 
 // ------------------------------------------------------------------------
 // element-wise pieces
 // ------------------------------------------------------------------------
-// a * z / |z|, with angle(0) = 0 -> a (np.angle(0) == 0, src/algorithms.py:30,33).
-// 1/sqrt(n2) to ~0.5 ulp: hardware estimate plus one Newton step (the
-// projection runs every iteration, so its rounding accumulates).
+// 1/sqrt(n2) to ~0.5 ulp of the compute type: the hardware float estimate plus
+// Newton steps (the projections run every iteration, their rounding accumulates).
 __device__ __forceinline__ float rsqrt_nr(float n2) {
     const float r = rsqrtf(n2);
     return fmaf(r * 0.5f, fmaf(-n2 * r, r, 1.0f), r);
 }
-__device__ __forceinline__ float2 unit_scale(float2 z, float a) {
-    const float n2 = z.x * z.x + z.y * z.y;
-    const bool zero = (n2 == 0.0f);  // select, not branch: no divergence in the unrolled loops
-    const float r = a * rsqrt_nr(zero ? 1.0f : n2);
-    return make_float2(zero ? a : z.x * r, zero ? 0.0f : z.y * r);
+__device__ __forceinline__ double rsqrt_nr(double n2) {
+    double r = (double)rsqrtf((float)n2);
+    r = fma(r * 0.5, fma(-n2 * r, r, 1.0), r);
+    r = fma(r * 0.5, fma(-n2 * r, r, 1.0), r);
+    return r;
 }
+// a * z / |z|, with angle(0) = 0 -> a (np.angle(0) == 0, src/algorithms.py:30,33).
+template <class C>
+__device__ __forceinline__ C unit_scale(C z, Scalar<C> a) {
+    using S = Scalar<C>;
+    const S n2 = z.x * z.x + z.y * z.y;
+    const bool zero = (n2 == (S)0);  // select, not branch: no divergence in the unrolled loops
+    const S r = a * rsqrt_nr(zero ? (S)1 : n2);
+    return mk<C>(zero ? a : z.x * r, zero ? (S)0 : z.y * r);
+}
+// x / |x| * a (src/algorithms.py:84); |x| = 0 gives NaN as in the reference
+template <class C>
+__device__ __forceinline__ C normalize(C x, Scalar<C> a) {
+    const Scalar<C> r = rsqrt_nr(x.x * x.x + x.y * x.y);
+    return mk<C>(x.x * r * a, x.y * r * a);
+}
+
+template <int P>
+using CplxOf = std::conditional_t<P == 0, float2, double2>;
 
 template <int TT>
 struct TgtLoad;
@@ -195,8 +215,10 @@ __device__ __forceinline__ void block_reduce_stats(double& mx, double& s2, doubl
 // ------------------------------------------------------------------------
 // row pass
 // ------------------------------------------------------------------------
-template <int W, int MODE>
+template <int W, int MODE, int P>
 __global__ void __launch_bounds__(RowCfg<W>::THREADS) row_kernel(RowParams p) {
+    using C = CplxOf<P>;
+    using S = Scalar<C>;
     constexpr int E = PlanOf<W>::E;
     constexpr int T = PlanOf<W>::T;
     constexpr int RPW = RowCfg<W>::RPW;
@@ -221,31 +243,29 @@ __global__ void __launch_bounds__(RowCfg<W>::THREADS) row_kernel(RowParams p) {
     const long long boff = hoff + blk_index(row, t, p.H);        // blocked (state), slot m adds m*T*H
     const long long bstep = (long long)T * p.H;
     const LdsLine lds{smem + lrow * LINE};
-    Twiddles<W, (RowCfg<W>::THREADS <= 512)> tw;
-    load_twiddles<W>(tw, t, p.tw);
-    float2 v[E];
+    Twiddles<W, C, (P == 0 && RowCfg<W>::THREADS <= 512)> tw;
+    load_twiddles<W, C>(tw, t, p.tw);
+    C v[E];
 
-    auto ain_at = [&](int m) -> float { return p.ain ? p.ain[roff + t + T * m] : 1.0f; };
+    auto ain_at = [&](int m) -> S { return p.ain ? (S)p.ain[roff + t + T * m] : (S)1; };
 
     if constexpr (MODE == ROW_PHASE_FWD) {
 #pragma unroll
         for (int m = 0; m < E; ++m) {
-            float s, c;
-            sincosf(p.phase_in[hoff + roff + t + T * m], &s, &c);
-            const float a = ain_at(m);
-            v[m] = make_float2(a * c, a * s);
+            S sn, cs;
+            if constexpr (P == 0)
+                sincosf(p.phase_in[hoff + roff + t + T * m], &sn, &cs);
+            else
+                sincos((double)p.phase_in[hoff + roff + t + T * m], &sn, &cs);
+            const S a = ain_at(m);
+            v[m] = mk<C>(a * cs, a * sn);
         }
     } else if constexpr (MODE == ROW_GD_INIT_FIELD) {
 #pragma unroll
-        for (int m = 0; m < E; ++m) {
-            const float2 x = p.field[boff + m * bstep];
-            const float a = ain_at(m);
-            const float r = rsqrt_nr(x.x * x.x + x.y * x.y);
-            v[m] = make_float2(x.x * r * a, x.y * r * a);
-        }
+        for (int m = 0; m < E; ++m) v[m] = normalize(from_c64<C>(p.field[boff + m * bstep]), ain_at(m));
     } else {
 #pragma unroll
-        for (int m = 0; m < E; ++m) v[m] = p.in[boff + m * bstep];
+        for (int m = 0; m < E; ++m) v[m] = from_c64<C>(p.in[boff + m * bstep]);
     }
     // the stop test is issued behind the loads so its latency overlaps them
     if constexpr (MODE == ROW_GS_MAIN) {
@@ -261,11 +281,11 @@ __global__ void __launch_bounds__(RowCfg<W>::THREADS) row_kernel(RowParams p) {
 
     if constexpr (MODE == ROW_GS_PHASE) {
 #pragma unroll
-        for (int m = 0; m < E; ++m) p.phase_out[hoff + roff + t + T * m] = atan2f(v[m].y, v[m].x);
+        for (int m = 0; m < E; ++m) p.phase_out[hoff + roff + t + T * m] = (float)atan2(v[m].y, v[m].x);
         return;
     } else if constexpr (MODE == ROW_FFT_INV) {
 #pragma unroll
-        for (int m = 0; m < E; ++m) p.out[boff + m * bstep] = v[m];
+        for (int m = 0; m < E; ++m) p.out[boff + m * bstep] = to_c64(v[m]);
         return;
     } else {
         if constexpr (MODE == ROW_GS_MAIN) {
@@ -274,46 +294,48 @@ __global__ void __launch_bounds__(RowCfg<W>::THREADS) row_kernel(RowParams p) {
         } else if constexpr (MODE == ROW_GD_INIT_Y) {
 #pragma unroll
             for (int m = 0; m < E; ++m) {
-                const float a = ain_at(m);
-                const float2 x = unit_scale(v[m], a);  // a_in exp(i angle(ifft2(sqrt T)))
-                p.field[boff + m * bstep] = x;
-                const float r = rsqrt_nr(x.x * x.x + x.y * x.y);
-                v[m] = make_float2(x.x * r * a, x.y * r * a);
+                const S a = ain_at(m);
+                const C x = unit_scale(v[m], a);  // a_in exp(i angle(ifft2(sqrt T)))
+                p.field[boff + m * bstep] = to_c64(x);
+                v[m] = normalize(x, a);
             }
         } else if constexpr (MODE == ROW_GD_MAIN) {
             // dEdF = ifft2(...) * a_in (src/algorithms.py:87-89); dEdX_complex (:179-185);
             // input -= lr * dEdX (:91); next forward input x/|x| a_in (:84).
-            const float lr = p.lr[p.iter];
+            const S lr = (S)p.lr[p.iter];
+            const S inv_s = (S)1 / (S)p.holo;
 #pragma unroll
             for (int m = 0; m < E; ++m) {
-                const float a = ain_at(m);
-                const float2 g = make_float2(v[m].x * p.inv_s * a, v[m].y * p.inv_s * a);
+                const S a = ain_at(m);
+                const C g = mk<C>(v[m].x * inv_s * a, v[m].y * inv_s * a);
                 const long long idx = boff + m * bstep;
-                float2 x = p.field[idx];
-                const float ax2 = x.x * x.x + x.y * x.y;
-                const float inv = 1.0f / sqrtf(ax2);
-                const float inv3 = inv * inv * inv;
-                const float re = x.x * g.x + x.y * g.y;
-                const float dx = g.x * inv - x.x * re * inv3;
-                const float dy = g.y * inv - x.y * re * inv3;
+                C x = from_c64<C>(p.field[idx]);
+                const S ax2 = x.x * x.x + x.y * x.y;
+                const S inv = rsqrt_nr(ax2);
+                const S inv3 = inv * inv * inv;
+                const S re = x.x * g.x + x.y * g.y;
+                const S dx = g.x * inv - x.x * re * inv3;
+                const S dy = g.y * inv - x.y * re * inv3;
                 x.x -= lr * dx;
                 x.y -= lr * dy;
-                p.field[idx] = x;
-                const float r = rsqrt_nr(x.x * x.x + x.y * x.y);
-                v[m] = make_float2(x.x * r * a, x.y * r * a);
+                const float2 xs = to_c64(x);  // the field is stored in complex64
+                p.field[idx] = xs;
+                v[m] = normalize(from_c64<C>(xs), a);
             }
         }
         fft_line<W, false>(v, t, tw, lds);
 #pragma unroll
-        for (int m = 0; m < E; ++m) p.out[boff + m * bstep] = v[m];
+        for (int m = 0; m < E; ++m) p.out[boff + m * bstep] = to_c64(v[m]);
     }
 }
 
 // ------------------------------------------------------------------------
 // column pass
 // ------------------------------------------------------------------------
-template <int H, int CW, int MODE, int TT>
+template <int H, int CW, int MODE, int TT, int P>
 __global__ void __launch_bounds__((ColCfg<H, CW>::THREADS)) col_kernel(ColParams p) {
+    using C = CplxOf<P>;
+    using S = Scalar<C>;
     constexpr int E = PlanOf<H>::E;
     constexpr int T = PlanOf<H>::T;
     constexpr int LINE = PlanOf<H>::LINE;
@@ -329,39 +351,39 @@ __global__ void __launch_bounds__((ColCfg<H, CW>::THREADS)) col_kernel(ColParams
     const long long base = (long long)b * p.holo + blk_index(t, x, H);
     constexpr long long kStep = 4LL * T;
     const LdsTile<CW> lds{smem, c};
-    Twiddles<H, (THREADS <= 512)> tw;
-    load_twiddles<H>(tw, t, p.tw);
-    float2 v[E];
+    Twiddles<H, C, (P == 0 && THREADS <= 512)> tw;
+    load_twiddles<H, C>(tw, t, p.tw);
+    C v[E];
 
     // GD gradient needs this iteration's global max of |F|^2 (src/algorithms.py:86).
-    float maxp = 0.0f;
+    S maxp = 0;
     if constexpr (MODE == COL_GD_GRAD) {
-        __shared__ float smax;
+        __shared__ double smax;
         const double* part = p.partials + ((long long)b * p.max_loops + p.iter) * p.nwg * 4;
         double m = 0.0;
         for (int k = threadIdx.x; k < p.nwg; k += THREADS) m = fmax(m, part[k * 4]);
         double d1 = 0.0, d2 = 0.0;
         block_reduce_stats<THREADS>(m, d1, d2);
-        if (threadIdx.x == 0) smax = (float)m;
+        if (threadIdx.x == 0) smax = m;
         __syncthreads();
-        maxp = smax;
+        maxp = (S)smax;
     }
 
     if constexpr (MODE == COL_REAL_INV) {
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             const float tv = TgtLoad<TT>::load(p.tgt, base + m * kStep);
-            v[m] = make_float2(TgtLoad<TT>::amp(tv), 0.0f);
+            v[m] = mk<C>((S)TgtLoad<TT>::amp(tv), (S)0);
         }
     } else if constexpr (MODE == COL_EXPECTED) {
         // GD keeps X of iteration i in buffer i % 2; GS passes the same buffer twice.
         const int s = min(p.stop_iter[b], p.loops - 1);
         const float2* src = (s & 1) ? p.in_alt : p.in;
 #pragma unroll
-        for (int m = 0; m < E; ++m) v[m] = src[base + m * kStep];
+        for (int m = 0; m < E; ++m) v[m] = from_c64<C>(src[base + m * kStep]);
     } else {
 #pragma unroll
-        for (int m = 0; m < E; ++m) v[m] = p.in[base + m * kStep];
+        for (int m = 0; m < E; ++m) v[m] = from_c64<C>(p.in[base + m * kStep]);
     }
     // the stop test is issued behind the loads so its latency overlaps them
     if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_STATS || MODE == COL_GD_GRAD) {
@@ -371,7 +393,7 @@ __global__ void __launch_bounds__((ColCfg<H, CW>::THREADS)) col_kernel(ColParams
     if constexpr (MODE == COL_REAL_INV || MODE == COL_FFT_INV) {
         fft_line<H, true>(v, t, tw, lds);
 #pragma unroll
-        for (int m = 0; m < E; ++m) p.out[base + m * kStep] = v[m];
+        for (int m = 0; m < E; ++m) p.out[base + m * kStep] = to_c64(v[m]);
         return;
     } else {
         fft_line<H, false>(v, t, tw, lds);
@@ -379,34 +401,35 @@ __global__ void __launch_bounds__((ColCfg<H, CW>::THREADS)) col_kernel(ColParams
 
     if constexpr (MODE == COL_FFT_FWD) {
 #pragma unroll
-        for (int m = 0; m < E; ++m) p.out[base + m * kStep] = v[m];
+        for (int m = 0; m < E; ++m) p.out[base + m * kStep] = to_c64(v[m]);
         return;
     } else if constexpr (MODE == COL_EXPECTED) {
         const long long nat = (long long)b * p.holo + (long long)t * p.W + x;  // row-major output
 #pragma unroll
         for (int m = 0; m < E; ++m)
-            p.e_out[nat + (long long)m * T * p.W] = v[m].x * v[m].x + v[m].y * v[m].y;
+            p.e_out[nat + (long long)m * T * p.W] = (float)(v[m].x * v[m].x + v[m].y * v[m].y);
         return;
     } else {
         double mx = 0.0, s2 = 0.0, st = 0.0;
-        const float norm = (MODE == COL_GD_GRAD) ? p.norm[b] : 0.0f;
+        const S norm = (MODE == COL_GD_GRAD) ? (S)p.norm[b] : (S)0;
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             const float tv = TgtLoad<TT>::load(p.tgt, base + m * kStep);
-            const float e = v[m].x * v[m].x + v[m].y * v[m].y;
+            const S e = v[m].x * v[m].x + v[m].y * v[m].y;
             if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_STATS) {
-                const double ed = (double)e;
+                // |C|^2 as the reference's float64 expected_outcome sees it
+                const double ed = (double)(float)e;
                 mx = fmax(mx, ed);
                 s2 += ed * ed;
                 st += ed * (double)tv;
             }
             if constexpr (MODE == COL_GS_MAIN) {
-                v[m] = unit_scale(v[m], TgtLoad<TT>::amp(tv));
+                v[m] = unit_scale(v[m], (S)TgtLoad<TT>::amp(tv));
             } else if constexpr (MODE == COL_GD_GRAD) {
                 // mask * F * (output - T), output = |F|^2 norm / max (src/algorithms.py:80,85-88)
-                const float o = e * norm / maxp;
-                const float w = (1.0f + p.wa * tv / 255.0f) * (o - tv);
-                v[m] = make_float2(v[m].x * w, v[m].y * w);
+                const S o = e * norm / maxp;
+                const S w = ((S)1 + (S)p.wa * (S)tv / (S)255) * (o - (S)tv);
+                v[m] = mk<C>(v[m].x * w, v[m].y * w);
             }
         }
         if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_STATS) {
@@ -422,7 +445,7 @@ __global__ void __launch_bounds__((ColCfg<H, CW>::THREADS)) col_kernel(ColParams
         if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD) {
             fft_line<H, true>(v, t, tw, lds);
 #pragma unroll
-            for (int m = 0; m < E; ++m) p.out[base + m * kStep] = v[m];
+            for (int m = 0; m < E; ++m) p.out[base + m * kStep] = to_c64(v[m]);
         }
     }
 }

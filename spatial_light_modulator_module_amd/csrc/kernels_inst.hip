@@ -14,22 +14,22 @@
 namespace slm {
 namespace {
 
-template <int N>
+template <int N, int P>
 RowFn row_table(int mode) {
     switch (mode) {
-        case ROW_GS_MAIN: return row_kernel<N, ROW_GS_MAIN>;
-        case ROW_GS_PHASE: return row_kernel<N, ROW_GS_PHASE>;
-        case ROW_PHASE_FWD: return row_kernel<N, ROW_PHASE_FWD>;
-        case ROW_GD_INIT_Y: return row_kernel<N, ROW_GD_INIT_Y>;
-        case ROW_GD_INIT_FIELD: return row_kernel<N, ROW_GD_INIT_FIELD>;
-        case ROW_GD_MAIN: return row_kernel<N, ROW_GD_MAIN>;
-        case ROW_FFT_FWD: return row_kernel<N, ROW_FFT_FWD>;
-        case ROW_FFT_INV: return row_kernel<N, ROW_FFT_INV>;
+        case ROW_GS_MAIN: return row_kernel<N, ROW_GS_MAIN, P>;
+        case ROW_GS_PHASE: return row_kernel<N, ROW_GS_PHASE, P>;
+        case ROW_PHASE_FWD: return row_kernel<N, ROW_PHASE_FWD, P>;
+        case ROW_GD_INIT_Y: return row_kernel<N, ROW_GD_INIT_Y, P>;
+        case ROW_GD_INIT_FIELD: return row_kernel<N, ROW_GD_INIT_FIELD, P>;
+        case ROW_GD_MAIN: return row_kernel<N, ROW_GD_MAIN, P>;
+        case ROW_FFT_FWD: return row_kernel<N, ROW_FFT_FWD, P>;
+        case ROW_FFT_INV: return row_kernel<N, ROW_FFT_INV, P>;
         default: return nullptr;
     }
 }
 
-template <int N, int CW>
+template <int N, int CW, int P>
 ColFn col_table_cw(int mode, int tt) {
     if constexpr (!ColCfg<N, CW>::kValid) {
         return nullptr;
@@ -37,32 +37,39 @@ ColFn col_table_cw(int mode, int tt) {
         const bool u8 = (tt == TGT_U8);
         switch (mode) {
             case COL_GS_MAIN:
-                return u8 ? col_kernel<N, CW, COL_GS_MAIN, TGT_U8> : col_kernel<N, CW, COL_GS_MAIN, TGT_F32>;
+                return u8 ? col_kernel<N, CW, COL_GS_MAIN, TGT_U8, P> : col_kernel<N, CW, COL_GS_MAIN, TGT_F32, P>;
             case COL_REAL_INV:
-                return u8 ? col_kernel<N, CW, COL_REAL_INV, TGT_U8> : col_kernel<N, CW, COL_REAL_INV, TGT_F32>;
+                return u8 ? col_kernel<N, CW, COL_REAL_INV, TGT_U8, P> : col_kernel<N, CW, COL_REAL_INV, TGT_F32, P>;
             case COL_GD_STATS:
-                return u8 ? col_kernel<N, CW, COL_GD_STATS, TGT_U8> : col_kernel<N, CW, COL_GD_STATS, TGT_F32>;
+                return u8 ? col_kernel<N, CW, COL_GD_STATS, TGT_U8, P> : col_kernel<N, CW, COL_GD_STATS, TGT_F32, P>;
             case COL_GD_GRAD:
-                return u8 ? col_kernel<N, CW, COL_GD_GRAD, TGT_U8> : col_kernel<N, CW, COL_GD_GRAD, TGT_F32>;
-            case COL_EXPECTED: return col_kernel<N, CW, COL_EXPECTED, TGT_F32>;
-            case COL_FFT_FWD: return col_kernel<N, CW, COL_FFT_FWD, TGT_F32>;
-            case COL_FFT_INV: return col_kernel<N, CW, COL_FFT_INV, TGT_F32>;
+                return u8 ? col_kernel<N, CW, COL_GD_GRAD, TGT_U8, P> : col_kernel<N, CW, COL_GD_GRAD, TGT_F32, P>;
+            case COL_EXPECTED: return col_kernel<N, CW, COL_EXPECTED, TGT_F32, P>;
+            case COL_FFT_FWD: return col_kernel<N, CW, COL_FFT_FWD, TGT_F32, P>;
+            case COL_FFT_INV: return col_kernel<N, CW, COL_FFT_INV, TGT_F32, P>;
             default: return nullptr;
         }
     }
 }
 
-}  // namespace
-
-RowFn SLM_PASTE(row_fn_, SLM_N)(int mode) { return row_table<SLM_N>(mode); }
-
-ColFn SLM_PASTE(col_fn_, SLM_N)(int cw, int mode, int tt) {
+template <int N, int P>
+ColFn col_table(int cw, int mode, int tt) {
     switch (cw) {
-        case 4: return col_table_cw<SLM_N, 4>(mode, tt);
-        case 8: return col_table_cw<SLM_N, 8>(mode, tt);
-        case 16: return col_table_cw<SLM_N, 16>(mode, tt);
+        case 4: return col_table_cw<N, 4, P>(mode, tt);
+        case 8: return col_table_cw<N, 8, P>(mode, tt);
+        case 16: return col_table_cw<N, 16, P>(mode, tt);
         default: return nullptr;
     }
+}
+
+}  // namespace
+
+RowFn SLM_PASTE(row_fn_, SLM_N)(int mode, int prec) {
+    return prec == PREC_F64 ? row_table<SLM_N, PREC_F64>(mode) : row_table<SLM_N, PREC_F32>(mode);
+}
+
+ColFn SLM_PASTE(col_fn_, SLM_N)(int cw, int mode, int tt, int prec) {
+    return prec == PREC_F64 ? col_table<SLM_N, PREC_F64>(cw, mode, tt) : col_table<SLM_N, PREC_F32>(cw, mode, tt);
 }
 
 int SLM_PASTE(row_threads_, SLM_N)() { return RowCfg<SLM_N>::THREADS; }

@@ -15,6 +15,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "../../include/slm_hip.h"
@@ -29,7 +30,7 @@ namespace {
 thread_local std::string g_err;
 int g_device = -1;
 std::mutex g_mu;
-std::map<std::pair<int, int>, float2*> g_twiddles;  // (device, n) -> table
+std::map<std::tuple<int, int, int>, void*> g_twiddles;  // (device, n, precision) -> table
 ncclComm_t g_comm = nullptr;
 int g_comm_rank = 0, g_comm_size = 1;
 
@@ -73,10 +74,11 @@ int ensure_device() {
 }
 
 // Twiddle table of one transform length, in the pass order of kPlans:
-// entry [(r - 1) * Ns + j] = exp(-2 pi i j r / (Ns R)), computed in double.
-int get_twiddles(int n, const float2** out) {
+// entry [(r - 1) * Ns + j] = exp(-2 pi i j r / (Ns R)), computed in double and
+// stored as float2 (PREC_F32) or double2 (PREC_F64).
+int get_twiddles(int n, int prec, const void** out) {
     std::lock_guard<std::mutex> lk(g_mu);
-    auto key = std::make_pair(g_device, n);
+    auto key = std::make_tuple(g_device, n, prec);
     auto it = g_twiddles.find(key);
     if (it != g_twiddles.end()) {
         *out = it->second;
@@ -85,8 +87,7 @@ int get_twiddles(int n, const float2** out) {
     const int pi = plan_index(n);
     if (pi < 0) return fail(SLM_ERR_UNSUPPORTED, "unsupported transform length %d", n);
     const RadixPlan& pl = kPlans[pi];
-    std::vector<float2> host;
-    host.reserve(twiddle_count(n) + 1);
+    std::vector<double> host;  // interleaved re, im
     int ns = 1;
     for (int k = 0; k < pl.npass; ++k) {
         const int r_ = pl.r[k];
@@ -96,15 +97,25 @@ int get_twiddles(int n, const float2** out) {
                 for (int j = 0; j < ns; ++j) {
                     const long long q = ((long long)j * r) % L;
                     const double ang = -2.0 * M_PI * (double)q / (double)L;
-                    host.push_back(make_float2((float)std::cos(ang), (float)std::sin(ang)));
+                    host.push_back(std::cos(ang));
+                    host.push_back(std::sin(ang));
                 }
         }
         ns *= r_;
     }
-    if (host.empty()) host.push_back(make_float2(1.f, 0.f));
-    float2* d = nullptr;
-    HIP_TRY(hipMalloc(&d, host.size() * sizeof(float2)));
-    HIP_TRY(hipMemcpy(d, host.data(), host.size() * sizeof(float2), hipMemcpyHostToDevice));
+    if (host.empty()) {
+        host.push_back(1.0);
+        host.push_back(0.0);
+    }
+    void* d = nullptr;
+    if (prec == PREC_F64) {
+        HIP_TRY(hipMalloc(&d, host.size() * sizeof(double)));
+        HIP_TRY(hipMemcpy(d, host.data(), host.size() * sizeof(double), hipMemcpyHostToDevice));
+    } else {
+        std::vector<float> f(host.begin(), host.end());
+        HIP_TRY(hipMalloc(&d, f.size() * sizeof(float)));
+        HIP_TRY(hipMemcpy(d, f.data(), f.size() * sizeof(float), hipMemcpyHostToDevice));
+    }
     g_twiddles[key] = d;
     *out = d;
     return 0;
@@ -171,8 +182,9 @@ struct slm_plan {
     int device = 0;
     long long holo = 0;
     hipStream_t stream = nullptr;
-    const float2* tw_row = nullptr;
-    const float2* tw_col = nullptr;
+    int prec = PREC_F64;
+    const void* tw_row = nullptr;
+    const void* tw_col = nullptr;
     float2 *xa = nullptr, *xb = nullptr, *y = nullptr, *field = nullptr;
     void* tgt = nullptr;
     float* ain = nullptr;
@@ -206,10 +218,10 @@ int pick_cw(int H, int W, int B) {
     (void)B;
     if (const char* s = std::getenv("SLM_COL_CW")) {
         const int cw = std::atoi(s);
-        if (col_fn(H, cw, COL_GS_MAIN, TGT_F32) && W % cw == 0) return cw;
+        if (col_fn(H, cw, COL_GS_MAIN, TGT_F32, PREC_F32) && W % cw == 0) return cw;
     }
     for (int cw : {4, 8, 16})
-        if (W % cw == 0 && col_fn(H, cw, COL_GS_MAIN, TGT_F32)) return cw;
+        if (W % cw == 0 && col_fn(H, cw, COL_GS_MAIN, TGT_F32, PREC_F32)) return cw;
     return 0;
 }
 
@@ -265,7 +277,7 @@ ColParams col_params(slm_plan* p) {
 }
 
 int launch_row(slm_plan* p, int mode, const RowParams& rp, int cls) {
-    RowFn fn = row_fn(p->W, mode);
+    RowFn fn = row_fn(p->W, mode, p->prec);
     if (!fn) return fail(SLM_ERR_UNSUPPORTED, "no row kernel for width %d mode %d", p->W, mode);
     int rc = begin_launch(p, cls);
     if (rc) return rc;
@@ -276,7 +288,7 @@ int launch_row(slm_plan* p, int mode, const RowParams& rp, int cls) {
 
 int launch_col(slm_plan* p, int mode, const ColParams& cp, int cls) {
     const int tt = (mode == COL_EXPECTED || mode == COL_FFT_FWD || mode == COL_FFT_INV) ? TGT_F32 : p->tt;
-    ColFn fn = col_fn(p->H, p->cw, mode, tt);
+    ColFn fn = col_fn(p->H, p->cw, mode, tt, p->prec);
     if (!fn) return fail(SLM_ERR_UNSUPPORTED, "no column kernel for height %d cw %d mode %d", p->H, p->cw, mode);
     int rc = begin_launch(p, cls);
     if (rc) return rc;
@@ -504,8 +516,9 @@ int slm_plan_create(int algo, int batch, int height, int width, int tgt_type, in
     p->col_threads = col_threads(height, p->cw);
     p->row_threads = row_threads(width);
     p->rpw = row_rpw(width);
-    int rc = get_twiddles(width, &p->tw_row);
-    if (!rc) rc = get_twiddles(height, &p->tw_col);
+    if (const char* e = std::getenv("SLM_PRECISION")) p->prec = (std::strcmp(e, "f32") == 0) ? PREC_F32 : PREC_F64;
+    int rc = get_twiddles(width, p->prec, &p->tw_row);
+    if (!rc) rc = get_twiddles(height, p->prec, &p->tw_col);
     if (rc) {
         delete p;
         return rc;
@@ -575,6 +588,22 @@ int slm_plan_set_target(slm_plan* p, const void* tgt) {
     p->target_set = true;
     return 0;
 }
+
+int slm_plan_set_precision(slm_plan* p, int precision) {
+    if (!p) return fail(SLM_ERR_ARG, "null plan");
+    if (precision != SLM_PRECISION_F32 && precision != SLM_PRECISION_F64)
+        return fail(SLM_ERR_ARG, "unknown precision %d", precision);
+    HIP_TRY(hipSetDevice(p->device));
+    const void *tr = nullptr, *tc = nullptr;
+    RC(get_twiddles(p->W, precision, &tr));
+    RC(get_twiddles(p->H, precision, &tc));
+    p->prec = precision;
+    p->tw_row = tr;
+    p->tw_col = tc;
+    return 0;
+}
+
+int slm_plan_get_precision(slm_plan* p) { return p ? p->prec : -1; }
 
 int slm_plan_set_ain(slm_plan* p, const float* ain) {
     if (!p || !ain) return fail(SLM_ERR_ARG, "null argument");

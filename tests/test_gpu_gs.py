@@ -61,10 +61,11 @@ def test_gs_incoming_intensity_uint8_vs_reference(gpu, golden_dir):
 @pytest.mark.gpu
 @pytest.mark.parametrize("shape", [(64, 128), (256, 256), (768, 1024), (512, 2048)])
 @pytest.mark.parametrize("dtype", [np.uint8, np.float32])
-def test_gs_matches_oracles(gpu, shape, dtype):
+def test_gs_matches_faithful_oracle(gpu, shape, dtype):
     """Warm start from a random phase (no Hermitian symmetry, so not chaotic):
-    the GPU tracks the float64 restatement of the reference within the phase
-    bound, and the complex64 model within float32 noise."""
+    the GPU (float64 butterflies, complex64 state) tracks the float64
+    restatement of the reference within the phase bound; a pure complex64
+    implementation lands 2.5e-6..1.0e-5 rms from it here."""
     from spatial_light_modulator_module_amd import algorithms as alg
 
     rng = np.random.default_rng(shape[0] * 7 + shape[1])
@@ -74,19 +75,12 @@ def test_gs_matches_oracles(gpu, shape, dtype):
     loops = 12
     phase, e, errs, norm, emax = alg.run_gs(t[None], loops, initial_phase=phi0[None])
     ph_f, exp_f, err_f = orc.gerchberg_saxton_faithful(t, loops, initial_phase=phi0.astype(np.float32))
-    ph_o, e_o, stats_o = orc.gerchberg_saxton_c64(t, loops, initial_phase=phi0)
-    # From a random phase the first loops are ill-conditioned wherever |C| is
-    # small; the complex64 model itself lands 2.5e-6..1.0e-5 rms from float64
-    # here, so the bound is the float32 floor (the reference-protocol test
-    # above holds the strict 1e-5).
-    floor = orc.phase_rms(ph_o, ph_f)
     rms = orc.phase_rms(phase[0], ph_f)
-    assert rms < max(PHASE_RMS_TOL, 1.5 * floor), f"rms {rms:.3e} vs float32 floor {floor:.3e}"
-    np.testing.assert_allclose(errs[0], err_f, rtol=1e-4)
-    assert orc.phase_rms(phase[0], ph_o) < 2 * max(PHASE_RMS_TOL, floor)
-    np.testing.assert_allclose(e[0], e_o, rtol=1e-3, atol=1e-4 * float(e_o.max()))
-    np.testing.assert_allclose(alg.expected_from(e[0], norm[0], emax[0]), exp_f, rtol=1e-3,
-                               atol=1e-4 * float(norm[0]))
+    print(f"[parity] GS {shape} {np.dtype(dtype).name} random warm start x{loops}: phase rms {rms:.3e}")
+    assert rms < PHASE_RMS_TOL
+    np.testing.assert_allclose(errs[0], err_f, rtol=1e-5)
+    np.testing.assert_allclose(alg.expected_from(e[0], norm[0], emax[0]), exp_f, rtol=1e-4,
+                               atol=1e-5 * float(norm[0]))
 
 
 @pytest.mark.gpu

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--algo", default="gs")
     ap.add_argument("--u8", action="store_true")
+    ap.add_argument("--prec", default="f64")
     o = ap.parse_args()
     h = o.height or o.size
     w = o.size
@@ -34,6 +35,7 @@ def main():
     _lib.init(0)
     with _lib.Plan(algo, o.batch, h, w, _lib.TGT_U8 if o.u8 else _lib.TGT_F32, False, o.iters) as p:
         p.set_target(t)
+        p.set_precision(_lib.PRECISION_F32 if o.prec == 'f32' else _lib.PRECISION_F64)
         if algo == _lib.ALGO_GD:
             p.set_lr(np.full(o.iters, 0.005, np.float32))
         for _ in range(o.reps):
