@@ -99,7 +99,9 @@ int slm_plan_read_target_stats(slm_plan* plan, double* norm, double* sum_t2);
 /* algorithmic HBM bytes moved by one launch of a kernel class */
 long long slm_plan_kernel_bytes(slm_plan* plan, int kernel_class);
 /* info[0] = column tile width, info[1] = column workgroups per hologram,
- * info[2] = column threads, info[3] = row threads, info[4] = rows per workgroup */
+ * info[2] = column threads, info[3] = row threads, info[4] = rows per workgroup,
+ * info[5] / info[6] = radix plan keys of rows / columns, info[7] = precision
+ * (info must hold 8 ints) */
 int slm_plan_info(slm_plan* plan, int* info);
 
 /* ---- one-shot helpers (upload, run, read) ------------------------------ */

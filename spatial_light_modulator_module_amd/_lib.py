@@ -11,7 +11,9 @@ import os
 
 import numpy as np
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libslm_hip.so")
+# $SLM_LIB_PATH selects an experimental build (A/B variants); default is the in-tree library
+LIB_PATH = os.environ.get("SLM_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib",
+                                                          "libslm_hip.so")
 
 ALGO_GS = 0
 ALGO_GD = 1
@@ -234,7 +236,8 @@ class Plan:
         a = np.zeros(8, np.int32)
         check(self._lib.slm_plan_info(self.handle, ptr(a)), "slm_plan_info")
         return {"col_cw": int(a[0]), "col_workgroups": int(a[1]), "col_threads": int(a[2]),
-                "row_threads": int(a[3]), "rows_per_workgroup": int(a[4])}
+                "row_threads": int(a[3]), "rows_per_workgroup": int(a[4]), "row_plan": int(a[5]),
+                "col_plan": int(a[6]), "precision": "f64" if a[7] == PRECISION_F64 else "f32"}
 
     def gather_phase(self, counts, root: int = 0, host_out: np.ndarray | None = None) -> None:
         c = np.ascontiguousarray(counts, dtype=np.int32)

@@ -1,6 +1,8 @@
-// Host-side lookup of the per-length kernel instantiations.
+// Host-side lookup of the per-plan kernel instantiations (keyed by plan key).
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include "plans.hpp"
 
 namespace slm {
 
@@ -16,16 +18,23 @@ using ColFn = void (*)(ColParams);
     int row_rpw_##N();                           \
     int col_threads_##N(int cw);
 
-SLM_DECLARE_LENGTH(64)
-SLM_DECLARE_LENGTH(128)
-SLM_DECLARE_LENGTH(256)
-SLM_DECLARE_LENGTH(512)
-SLM_DECLARE_LENGTH(768)
-SLM_DECLARE_LENGTH(1024)
-SLM_DECLARE_LENGTH(2048)
-SLM_DECLARE_LENGTH(4096)
+SLM_DECLARE_LENGTH(0)
+SLM_DECLARE_LENGTH(1)
+SLM_DECLARE_LENGTH(2)
+SLM_DECLARE_LENGTH(3)
+SLM_DECLARE_LENGTH(4)
+SLM_DECLARE_LENGTH(5)
+SLM_DECLARE_LENGTH(6)
+SLM_DECLARE_LENGTH(7)
+SLM_DECLARE_LENGTH(8)
+SLM_DECLARE_LENGTH(9)
+SLM_DECLARE_LENGTH(10)
+SLM_DECLARE_LENGTH(11)
+SLM_DECLARE_LENGTH(12)
 
-#define SLM_FOR_EACH_LENGTH(X) X(64) X(128) X(256) X(512) X(768) X(1024) X(2048) X(4096)
+// plan keys (indices into kPlans); the Makefile builds one object per key
+static_assert(kNumPlans == 13, "update SLM_DECLARE_LENGTH / SLM_FOR_EACH_LENGTH and the Makefile");
+#define SLM_FOR_EACH_LENGTH(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12)
 
 inline RowFn row_fn(int n, int mode, int prec) {
 #define SLM_CASE(N) \

@@ -45,17 +45,19 @@ __device__ __forceinline__ void static_for(F&& f) {
     static_for_impl<0, N>(f);
 }
 
-template <int N, std::size_t... I>
+// Templates below take a plan key K (index into kPlans, plans.hpp).
+template <int K, std::size_t... I>
 constexpr auto radices_of(std::index_sequence<I...>) {
-    return IntList<kPlans[plan_index(N)].r[I]...>{};
+    return IntList<kPlans[K].r[I]...>{};
 }
-template <int N>
-using RadicesOf = decltype(radices_of<N>(std::make_index_sequence<kPlans[plan_index(N)].npass>{}));
+template <int K>
+using RadicesOf = decltype(radices_of<K>(std::make_index_sequence<kPlans[K].npass>{}));
 
-template <int N>
+template <int K>
 struct PlanOf {
-    static_assert(plan_index(N) >= 0, "unsupported transform length");
-    static constexpr int E = kPlans[plan_index(N)].e;
+    static_assert(K >= 0 && K < kNumPlans, "unknown plan key");
+    static constexpr int N = kPlans[K].n;
+    static constexpr int E = kPlans[K].e;
     static constexpr int T = N / E;
     static constexpr int LINE = lds_line(N);
     // row stride of per-row LDS regions: == 16 (mod 32) complex, so the two rows
@@ -236,18 +238,31 @@ struct Dft<16, INV, C> {
 // t + T m of the line; padding one slot per 16 keeps the strided first-pass
 // writes off a single bank.
 // ------------------------------------------------------------------------
+// X = float2 or double2: the element type of the exchange (float64 exchanges
+// avoid two conversions per element and pass where the LDS budget allows).
+template <class X>
 struct LdsLine {  // one transform line per thread group (row kernels)
-    float2* base;
-    __device__ __forceinline__ void store(int o, float2 v) const { base[o + (o >> 4)] = v; }
-    __device__ __forceinline__ float2 load(int o) const { return base[o + (o >> 4)]; }
+    X* base;
+    template <class C>
+    __device__ __forceinline__ void store(int o, C v) const { base[o + (o >> 4)] = mk<X>(v.x, v.y); }
+    template <class C>
+    __device__ __forceinline__ C load(int o) const {
+        const X v = base[o + (o >> 4)];
+        return mk<C>(v.x, v.y);
+    }
 };
 
-template <int CW>
+template <int CW, class X>
 struct LdsTile {  // CW interleaved columns (column kernels): [o][c]
-    float2* base;
+    X* base;
     int c;
-    __device__ __forceinline__ void store(int o, float2 v) const { base[(o + (o >> 4)) * CW + c] = v; }
-    __device__ __forceinline__ float2 load(int o) const { return base[(o + (o >> 4)) * CW + c]; }
+    template <class C>
+    __device__ __forceinline__ void store(int o, C v) const { base[(o + (o >> 4)) * CW + c] = mk<X>(v.x, v.y); }
+    template <class C>
+    __device__ __forceinline__ C load(int o) const {
+        const X v = base[(o + (o >> 4)) * CW + c];
+        return mk<C>(v.x, v.y);
+    }
 };
 
 // ------------------------------------------------------------------------
@@ -274,65 +289,145 @@ struct TwCountOf<N, IntList<Rs...>> {
     static constexpr int value = TwCountImpl<N, 1, Rs...>::value;
 };
 
-// CACHED: every twiddle of the thread in registers (one load each per kernel).
-// !CACHED: read from the (L1/L2-resident) table where used — when the
-// register budget of the workgroup cannot hold the cache.
-template <int N, class C, bool CACHED>
-struct Twiddles {
+// Twiddle sources (TwMode):
+//  TW_CACHED: every twiddle of the thread in registers, one table load each per
+//             kernel (float32 arithmetic: exact table values matter there);
+//  TW_DIRECT: read from the (L1/L2-resident) table where used, for 1024-thread
+//             workgroups whose 128-VGPR budget cannot hold a cache;
+//  TW_POWERS: float64 arithmetic: only w^1 of each butterfly is cached and the
+//             powers w^2..w^(R-1) are formed by multiplication (error ~1e-15,
+//             far below the complex64 storage rounding).
+enum TwMode : int { TW_CACHED = 0, TW_DIRECT = 1, TW_POWERS = 2 };
+
+template <int N, int Ns, int... Rs>
+struct TwPowCountImpl;
+template <int N, int Ns>
+struct TwPowCountImpl<N, Ns> {
+    static constexpr int value = 0;
+};
+template <int N, int Ns, int R, int... Rest>
+struct TwPowCountImpl<N, Ns, R, Rest...> {
+    static constexpr int value = (Ns > 1 ? PlanOf<N>::E / R : 0) + TwPowCountImpl<N, Ns * R, Rest...>::value;
+};
+template <int N, class L>
+struct TwPowCountOf;
+template <int N, int... Rs>
+struct TwPowCountOf<N, IntList<Rs...>> {
+    static constexpr int value = TwPowCountImpl<N, 1, Rs...>::value;
+};
+
+// w[r] = w^r for r = 1..R-1 from w[1], log-depth (w^(2k) = (w^k)^2, else
+// w^hi * w^(r-hi) with hi the highest power of two below r)
+template <int R, class C>
+__device__ __forceinline__ void twiddle_powers(C (&w)[R]) {
+    static_for<R - 2>([&](auto rc) {
+        constexpr int r = decltype(rc)::value + 2;
+        constexpr int hi = (r & (r - 1)) == 0 ? r / 2 : (1 << (31 - __builtin_clz(r)));
+        constexpr int lo = (r & (r - 1)) == 0 ? r / 2 : r - hi;
+        w[r] = cmul(w[hi], w[lo]);
+    });
+}
+
+template <int N, class C, int MODE>
+struct Twiddles;
+
+template <int N, class C>
+struct Twiddles<N, C, TW_CACHED> {
     static constexpr int COUNT = TwCountOf<N, RadicesOf<N>>::value > 0 ? TwCountOf<N, RadicesOf<N>>::value : 1;
     C w[COUNT];
-    template <int TwOff, int RegOff, int R, int Ns>
-    __device__ __forceinline__ C get(int k, int r, int) const {
-        return w[RegOff + k * (R - 1) + r - 1];
+    template <int TwOff, int RegOff, int PowOff, int R, int Ns, bool INV>
+    __device__ __forceinline__ void apply(C* u, int k, int) const {
+        static_for<R - 1>([&](auto rc) {
+            constexpr int r = decltype(rc)::value + 1;
+            const C t = w[RegOff + k * (R - 1) + r - 1];
+            u[r] = INV ? cmulc(u[r], t) : cmul(u[r], t);
+        });
     }
 };
 template <int N, class C>
-struct Twiddles<N, C, false> {
+struct Twiddles<N, C, TW_DIRECT> {
     const C* __restrict__ table;
-    template <int TwOff, int RegOff, int R, int Ns>
-    __device__ __forceinline__ C get(int, int r, int j) const {
-        return table[TwOff + (r - 1) * Ns + j];
+    template <int TwOff, int RegOff, int PowOff, int R, int Ns, bool INV>
+    __device__ __forceinline__ void apply(C* u, int, int j) const {
+        static_for<R - 1>([&](auto rc) {
+            constexpr int r = decltype(rc)::value + 1;
+            const C t = table[TwOff + (r - 1) * Ns + j];
+            u[r] = INV ? cmulc(u[r], t) : cmul(u[r], t);
+        });
+    }
+};
+template <int N, class C>
+struct Twiddles<N, C, TW_POWERS> {
+    static constexpr int COUNT = TwPowCountOf<N, RadicesOf<N>>::value > 0 ? TwPowCountOf<N, RadicesOf<N>>::value : 1;
+    C w1[COUNT];
+    template <int TwOff, int RegOff, int PowOff, int R, int Ns, bool INV>
+    __device__ __forceinline__ void apply(C* u, int k, int) const {
+        C w[R];
+        w[1] = w1[PowOff + k];
+        twiddle_powers<R>(w);
+        static_for<R - 1>([&](auto rc) {
+            constexpr int r = decltype(rc)::value + 1;
+            u[r] = INV ? cmulc(u[r], w[r]) : cmul(u[r], w[r]);
+        });
     }
 };
 
-template <int N, class C, int E, int Ns, int TwOff, int RegOff, int R, int... Rest>
-__device__ __forceinline__ void load_twiddles_pass(Twiddles<N, C, true>& tw, int t, const C* __restrict__ table) {
-    constexpr int T = N / E;
+template <int N, class C, int MODE, int E, int Ns, int TwOff, int RegOff, int PowOff, int R, int... Rest>
+__device__ __forceinline__ void load_twiddles_pass(Twiddles<N, C, MODE>& tw, int t, const C* __restrict__ table) {
+    constexpr int T = PlanOf<N>::T;  // N is the plan key here
     constexpr int NB = E / R;
     if constexpr (Ns > 1) {
         static_for<NB>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
             const int j = (t + k * T) % Ns;
-            static_for<R - 1>([&](auto rc) {
-                constexpr int r = decltype(rc)::value;
-                tw.w[RegOff + k * (R - 1) + r] = table[TwOff + r * Ns + j];
-            });
+            if constexpr (MODE == TW_CACHED) {
+                static_for<R - 1>([&](auto rc) {
+                    constexpr int r = decltype(rc)::value;
+                    tw.w[RegOff + k * (R - 1) + r] = table[TwOff + r * Ns + j];
+                });
+            } else {
+                tw.w1[PowOff + k] = table[TwOff + j];  // r = 1 entry
+            }
         });
     }
     if constexpr (sizeof...(Rest) > 0) {
         constexpr int kNextOff = TwOff + (Ns > 1 ? (R - 1) * Ns : 0);
         constexpr int kNextReg = RegOff + (Ns > 1 ? NB * (R - 1) : 0);
-        load_twiddles_pass<N, C, E, Ns * R, kNextOff, kNextReg, Rest...>(tw, t, table);
+        constexpr int kNextPow = PowOff + (Ns > 1 ? NB : 0);
+        load_twiddles_pass<N, C, MODE, E, Ns * R, kNextOff, kNextReg, kNextPow, Rest...>(tw, t, table);
     }
 }
-template <int N, class C, int... Rs>
-__device__ __forceinline__ void load_twiddles_impl(Twiddles<N, C, true>& tw, int t, const C* table, IntList<Rs...>) {
-    load_twiddles_pass<N, C, PlanOf<N>::E, 1, 0, 0, Rs...>(tw, t, table);
+template <int N, class C, int MODE, int... Rs>
+__device__ __forceinline__ void load_twiddles_impl(Twiddles<N, C, MODE>& tw, int t, const C* table, IntList<Rs...>) {
+    load_twiddles_pass<N, C, MODE, PlanOf<N>::E, 1, 0, 0, 0, Rs...>(tw, t, table);
 }
-template <int N, class C>
-__device__ __forceinline__ void load_twiddles(Twiddles<N, C, true>& tw, int t, const void* table) {
-    load_twiddles_impl<N, C>(tw, t, static_cast<const C*>(table), RadicesOf<N>{});
+template <int N, class C, int MODE>
+__device__ __forceinline__ void load_twiddles(Twiddles<N, C, MODE>& tw, int t, const void* table) {
+    if constexpr (MODE == TW_DIRECT)
+        tw.table = static_cast<const C*>(table);
+    else
+        load_twiddles_impl<N, C, MODE>(tw, t, static_cast<const C*>(table), RadicesOf<N>{});
 }
-template <int N, class C>
-__device__ __forceinline__ void load_twiddles(Twiddles<N, C, false>& tw, int, const void* table) {
-    tw.table = static_cast<const C*>(table);
+
+// Workgroup barrier for the LDS exchanges. __syncthreads() alone did not stop
+// hipcc (ROCm 7.2, 1024-thread workgroups under the 128-VGPR cap) from sinking
+// the exchange's ds_reads below the following barrier, so a fast wave's next
+// pass overwrote LDS a slow wave had not read yet (a ~1.5 % per-launch race).
+// The memory clobbers and sched_barrier pin every LDS access to its side.
+__device__ __forceinline__ void exchange_barrier() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
 }
 
 // ------------------------------------------------------------------------
 // Stockham driver. v[m] holds element t + T m on entry and the transform's
 // element t + T m on exit.
 // ------------------------------------------------------------------------
-template <int N, int E, bool INV, int Ns, int TwOff, int RegOff, class C, class Lds, class Tw, int R, int... Rest>
+template <int N, int E, bool INV, int Ns, int TwOff, int RegOff, int PowOff, class C, class Lds, class Tw, int R,
+          int... Rest>
 __device__ __forceinline__ void stockham_pass(C (&v)[E], int t, const Tw& tw, const Lds& lds) {
     constexpr int T = N / E;
     constexpr int NB = E / R;
@@ -346,13 +441,7 @@ __device__ __forceinline__ void stockham_pass(C (&v)[E], int t, const Tw& tw, co
             constexpr int r = decltype(rc)::value;
             u[r] = v[k + r * NB];
         });
-        if constexpr (Ns > 1) {
-            static_for<R - 1>([&](auto rc) {
-                constexpr int r = decltype(rc)::value + 1;
-                const C w = tw.template get<TwOff, RegOff, R, Ns>(k, r, j);
-                u[r] = INV ? cmulc(u[r], w) : cmul(u[r], w);
-            });
-        }
+        if constexpr (Ns > 1) tw.template apply<TwOff, RegOff, PowOff, R, Ns, INV>(u, k, j);
         Dft<R, INV, C>::run(u);
         if constexpr (sizeof...(Rest) == 0) {
             // last pass: Ns * R == N, so b < Ns and output r lands in slot k + r NB
@@ -364,34 +453,35 @@ __device__ __forceinline__ void stockham_pass(C (&v)[E], int t, const Tw& tw, co
             const int o = (b / Ns) * Ns * R + j;
             static_for<R>([&](auto rc) {
                 constexpr int r = decltype(rc)::value;
-                lds.store(o + r * Ns, to_c64(u[r]));
+                lds.store(o + r * Ns, u[r]);
             });
         }
     });
     if constexpr (sizeof...(Rest) > 0) {
-        __syncthreads();
+        exchange_barrier();
         static_for<E>([&](auto mc) {
             constexpr int m = decltype(mc)::value;
-            v[m] = from_c64<C>(lds.load(t + m * T));
+            v[m] = lds.template load<C>(t + m * T);
         });
-        __syncthreads();
+        exchange_barrier();
         constexpr int kNextReg = RegOff + (Ns > 1 ? NB * (R - 1) : 0);
         constexpr int kNextOff = TwOff + (Ns > 1 ? (R - 1) * Ns : 0);
-        stockham_pass<N, E, INV, Ns * R, kNextOff, kNextReg, C, Lds, Tw, Rest...>(v, t, tw, lds);
+        constexpr int kNextPow = PowOff + (Ns > 1 ? NB : 0);
+        stockham_pass<N, E, INV, Ns * R, kNextOff, kNextReg, kNextPow, C, Lds, Tw, Rest...>(v, t, tw, lds);
     }
 }
 
-template <int N, bool INV, class C, class Lds, class Tw, int... Rs>
-__device__ __forceinline__ void fft_line_impl(C (&v)[PlanOf<N>::E], int t, const Tw& tw, const Lds& lds,
+template <int K, bool INV, class C, class Lds, class Tw, int... Rs>
+__device__ __forceinline__ void fft_line_impl(C (&v)[PlanOf<K>::E], int t, const Tw& tw, const Lds& lds,
                                               IntList<Rs...>) {
-    stockham_pass<N, PlanOf<N>::E, INV, 1, 0, 0, C, Lds, Tw, Rs...>(v, t, tw, lds);
+    stockham_pass<PlanOf<K>::N, PlanOf<K>::E, INV, 1, 0, 0, 0, C, Lds, Tw, Rs...>(v, t, tw, lds);
 }
 
 // Transform one line held in the slot layout. Every thread of the workgroup
 // must call this (it contains workgroup barriers).
-template <int N, bool INV, class C, class Lds, class Tw>
-__device__ __forceinline__ void fft_line(C (&v)[PlanOf<N>::E], int t, const Tw& tw, const Lds& lds) {
-    fft_line_impl<N, INV, C>(v, t, tw, lds, RadicesOf<N>{});
+template <int K, bool INV, class C, class Lds, class Tw>
+__device__ __forceinline__ void fft_line(C (&v)[PlanOf<K>::E], int t, const Tw& tw, const Lds& lds) {
+    fft_line_impl<K, INV, C>(v, t, tw, lds, RadicesOf<K>{});
 }
 
 }  // namespace slm

@@ -100,18 +100,19 @@ enum Precision : int { PREC_F32 = 0, PREC_F64 = 1, PREC_NUM = 2 };
 // ------------------------------------------------------------------------
 // geometry
 // ------------------------------------------------------------------------
-template <int W>
+template <int K>  // plan key of the row length
 struct RowCfg {
-    static constexpr int T = PlanOf<W>::T;
+    static constexpr int T = PlanOf<K>::T;
     static constexpr int RPW = (T >= 64) ? 4 : 256 / T;  // rows per workgroup, a multiple of 4
     static constexpr int THREADS = RPW * T;
 };
 
-template <int H, int CW>
+template <int K, int CW>  // plan key of the column length
 struct ColCfg {
-    static constexpr int T = PlanOf<H>::T;
+    static constexpr int T = PlanOf<K>::T;
     static constexpr int THREADS = CW * T;
-    static constexpr bool kValid = THREADS >= 64 && THREADS <= 1024 && lds_line(H) * CW * 8 <= 160 * 1024;
+    static constexpr bool kValid =
+        THREADS >= 64 && THREADS <= 1024 && lds_line(PlanOf<K>::N) * CW * 8 <= 160 * 1024;
 };
 
 // XCD-aware bijective remap: blocks that share (id % 8) — one XCD under the
@@ -143,10 +144,10 @@ __device__ __forceinline__ float rsqrt_nr(float n2) {
     return fmaf(r * 0.5f, fmaf(-n2 * r, r, 1.0f), r);
 }
 __device__ __forceinline__ double rsqrt_nr(double n2) {
-    double r = (double)rsqrtf((float)n2);
-    r = fma(r * 0.5, fma(-n2 * r, r, 1.0), r);
-    r = fma(r * 0.5, fma(-n2 * r, r, 1.0), r);
-    return r;
+    // one step from the float estimate: ~1e-14 relative, far below the
+    // complex64 rounding of every stored value
+    const double r = (double)rsqrtf((float)n2);
+    return fma(r * 0.5, fma(-n2 * r, r, 1.0), r);
 }
 // a * z / |z|, with angle(0) = 0 -> a (np.angle(0) == 0, src/algorithms.py:30,33).
 template <class C>
@@ -166,6 +167,25 @@ __device__ __forceinline__ C normalize(C x, Scalar<C> a) {
 
 template <int P>
 using CplxOf = std::conditional_t<P == 0, float2, double2>;
+
+// exchange in the compute type when that keeps the workgroup's LDS <= 80 KiB
+// (two workgroups per CU), otherwise in complex64
+#ifndef SLM_F64_XCHG
+#define SLM_F64_XCHG 0
+#endif
+#ifndef SLM_F64_TW
+#define SLM_F64_TW TW_DIRECT
+#endif
+// float64 exchanges: narrow plans (more passes, hence more exchange roundings,
+// used for single small images where LDS is plentiful) and SLM_F64_XCHG builds
+template <int P, long long SLOTS, int K>
+using XchgOf = std::conditional_t<((SLM_F64_XCHG || kPlans[K].variant == 1) && P == 1 && SLOTS * 16 <= 80 * 1024),
+                                  double2, float2>;
+
+template <int P, int THREADS>
+constexpr int tw_mode() {
+    return P == 1 ? SLM_F64_TW : (THREADS <= 512 ? TW_CACHED : TW_DIRECT);
+}
 
 template <int TT>
 struct TgtLoad;
@@ -215,16 +235,18 @@ __device__ __forceinline__ void block_reduce_stats(double& mx, double& s2, doubl
 // ------------------------------------------------------------------------
 // row pass
 // ------------------------------------------------------------------------
-template <int W, int MODE, int P>
-__global__ void __launch_bounds__(RowCfg<W>::THREADS) row_kernel(RowParams p) {
+template <int K, int MODE, int P>
+__global__ void __launch_bounds__(RowCfg<K>::THREADS) row_kernel(RowParams p) {
     using C = CplxOf<P>;
     using S = Scalar<C>;
-    constexpr int E = PlanOf<W>::E;
-    constexpr int T = PlanOf<W>::T;
-    constexpr int RPW = RowCfg<W>::RPW;
-    constexpr int LINE = PlanOf<W>::ROWSTRIDE;
+    constexpr int W = PlanOf<K>::N;
+    constexpr int E = PlanOf<K>::E;
+    constexpr int T = PlanOf<K>::T;
+    constexpr int RPW = RowCfg<K>::RPW;
+    constexpr int LINE = PlanOf<K>::ROWSTRIDE;
     constexpr int TL = T < 16 ? T : 16;
-    __shared__ float2 smem[RPW * LINE];
+    using X = XchgOf<P, (long long)RPW * LINE, K>;
+    __shared__ X smem[RPW * LINE];
 
     const int b = blockIdx.y;
     // lane -> (row within the quad, transform thread t): TL consecutive t of
@@ -242,9 +264,9 @@ __global__ void __launch_bounds__(RowCfg<W>::THREADS) row_kernel(RowParams p) {
     const long long roff = (long long)row * W;                  // row-major (user arrays)
     const long long boff = hoff + blk_index(row, t, p.H);        // blocked (state), slot m adds m*T*H
     const long long bstep = (long long)T * p.H;
-    const LdsLine lds{smem + lrow * LINE};
-    Twiddles<W, C, (P == 0 && RowCfg<W>::THREADS <= 512)> tw;
-    load_twiddles<W, C>(tw, t, p.tw);
+    const LdsLine<X> lds{smem + lrow * LINE};
+    Twiddles<K, C, tw_mode<P, RowCfg<K>::THREADS>()> tw;
+    load_twiddles<K, C>(tw, t, p.tw);
     C v[E];
 
     auto ain_at = [&](int m) -> S { return p.ain ? (S)p.ain[roff + t + T * m] : (S)1; };
@@ -276,7 +298,7 @@ __global__ void __launch_bounds__(RowCfg<W>::THREADS) row_kernel(RowParams p) {
 
     if constexpr (MODE == ROW_GS_MAIN || MODE == ROW_GS_PHASE || MODE == ROW_GD_INIT_Y || MODE == ROW_GD_MAIN ||
                   MODE == ROW_FFT_INV) {
-        fft_line<W, true>(v, t, tw, lds);
+        fft_line<K, true>(v, t, tw, lds);
     }
 
     if constexpr (MODE == ROW_GS_PHASE) {
@@ -323,7 +345,7 @@ __global__ void __launch_bounds__(RowCfg<W>::THREADS) row_kernel(RowParams p) {
                 v[m] = normalize(from_c64<C>(xs), a);
             }
         }
-        fft_line<W, false>(v, t, tw, lds);
+        fft_line<K, false>(v, t, tw, lds);
 #pragma unroll
         for (int m = 0; m < E; ++m) p.out[boff + m * bstep] = to_c64(v[m]);
     }
@@ -332,15 +354,17 @@ __global__ void __launch_bounds__(RowCfg<W>::THREADS) row_kernel(RowParams p) {
 // ------------------------------------------------------------------------
 // column pass
 // ------------------------------------------------------------------------
-template <int H, int CW, int MODE, int TT, int P>
-__global__ void __launch_bounds__((ColCfg<H, CW>::THREADS)) col_kernel(ColParams p) {
+template <int K, int CW, int MODE, int TT, int P>
+__global__ void __launch_bounds__((ColCfg<K, CW>::THREADS)) col_kernel(ColParams p) {
     using C = CplxOf<P>;
     using S = Scalar<C>;
-    constexpr int E = PlanOf<H>::E;
-    constexpr int T = PlanOf<H>::T;
-    constexpr int LINE = PlanOf<H>::LINE;
-    constexpr int THREADS = ColCfg<H, CW>::THREADS;
-    __shared__ float2 smem[LINE * CW];
+    constexpr int H = PlanOf<K>::N;
+    constexpr int E = PlanOf<K>::E;
+    constexpr int T = PlanOf<K>::T;
+    constexpr int LINE = PlanOf<K>::LINE;
+    constexpr int THREADS = ColCfg<K, CW>::THREADS;
+    using X = XchgOf<P, (long long)LINE * CW, K>;
+    __shared__ X smem[LINE * CW];
 
     const int b = blockIdx.y;
     const int wg = xcd_remap(blockIdx.x, gridDim.x);
@@ -350,9 +374,9 @@ __global__ void __launch_bounds__((ColCfg<H, CW>::THREADS)) col_kernel(ColParams
     // blocked layout: element (y, x) at blk_index(y, x, H); row y = t + T m
     const long long base = (long long)b * p.holo + blk_index(t, x, H);
     constexpr long long kStep = 4LL * T;
-    const LdsTile<CW> lds{smem, c};
-    Twiddles<H, C, (P == 0 && THREADS <= 512)> tw;
-    load_twiddles<H, C>(tw, t, p.tw);
+    const LdsTile<CW, X> lds{smem, c};
+    Twiddles<K, C, tw_mode<P, THREADS>()> tw;
+    load_twiddles<K, C>(tw, t, p.tw);
     C v[E];
 
     // GD gradient needs this iteration's global max of |F|^2 (src/algorithms.py:86).
@@ -391,12 +415,12 @@ __global__ void __launch_bounds__((ColCfg<H, CW>::THREADS)) col_kernel(ColParams
     }
 
     if constexpr (MODE == COL_REAL_INV || MODE == COL_FFT_INV) {
-        fft_line<H, true>(v, t, tw, lds);
+        fft_line<K, true>(v, t, tw, lds);
 #pragma unroll
         for (int m = 0; m < E; ++m) p.out[base + m * kStep] = to_c64(v[m]);
         return;
     } else {
-        fft_line<H, false>(v, t, tw, lds);
+        fft_line<K, false>(v, t, tw, lds);
     }
 
     if constexpr (MODE == COL_FFT_FWD) {
@@ -443,7 +467,7 @@ __global__ void __launch_bounds__((ColCfg<H, CW>::THREADS)) col_kernel(ColParams
             }
         }
         if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD) {
-            fft_line<H, true>(v, t, tw, lds);
+            fft_line<K, true>(v, t, tw, lds);
 #pragma unroll
             for (int m = 0; m < E; ++m) p.out[base + m * kStep] = to_c64(v[m]);
         }

@@ -1,11 +1,11 @@
-// Instantiates every row / column kernel for one transform length SLM_N.
-// Compiled once per supported length (see Makefile) so the builds run in
-// parallel; dispatch.hip maps (length, mode, ...) to these tables.
+// Instantiates every row / column kernel of one radix plan (plan key SLM_N,
+// an index into kPlans). Compiled once per plan (see Makefile) so the builds
+// run in parallel; dispatch.hpp maps (plan key, mode, ...) to these tables.
 #include "dispatch.hpp"
 #include "kernels.hpp"
 
 #ifndef SLM_N
-#error "compile with -DSLM_N=<length>"
+#error "compile with -DSLM_N=<plan key>"
 #endif
 
 #define SLM_PASTE2(a, b) a##b

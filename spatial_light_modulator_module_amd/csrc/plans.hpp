@@ -14,39 +14,46 @@ namespace slm {
 struct RadixPlan {
     int n;        // transform length
     int e;        // complex elements held per thread
+    int variant;  // 0 = wide (16-24 elements per thread), 1 = narrow (twice the threads)
     int npass;    // number of Stockham passes
     int r[4];     // radices, first pass first
 };
 
 // Lengths the library supports along either image axis. 768 = 3 * 256 is the
 // SLM height of the reference CLI (src/constants.py:5-6).
+// Kernel templates are keyed by the index into this table (the "plan key").
+// Wide plans minimise passes; narrow plans halve the work per thread so a
+// single small image still puts several waves on every SIMD.
 constexpr RadixPlan kPlans[] = {
-    {64, 8, 2, {8, 8, 0, 0}},
-    {128, 16, 2, {16, 8, 0, 0}},
-    {256, 16, 2, {16, 16, 0, 0}},
-    {512, 16, 3, {16, 16, 2, 0}},
-    {768, 24, 3, {12, 8, 8, 0}},
-    {1024, 16, 3, {16, 16, 4, 0}},
-    {2048, 16, 3, {16, 16, 8, 0}},
-    {4096, 16, 3, {16, 16, 16, 0}},
+    {64, 8, 0, 2, {8, 8, 0, 0}},
+    {128, 16, 0, 2, {16, 8, 0, 0}},
+    {256, 16, 0, 2, {16, 16, 0, 0}},
+    {512, 16, 0, 3, {16, 16, 2, 0}},
+    {768, 24, 0, 3, {12, 8, 8, 0}},
+    {1024, 16, 0, 3, {16, 16, 4, 0}},
+    {2048, 16, 0, 3, {16, 16, 8, 0}},
+    {4096, 16, 0, 3, {16, 16, 16, 0}},
+    {256, 8, 1, 3, {8, 8, 4, 0}},
+    {512, 8, 1, 3, {8, 8, 8, 0}},
+    {768, 12, 1, 4, {12, 4, 4, 4}},
+    {1024, 8, 1, 4, {8, 8, 4, 4}},
+    {2048, 8, 1, 4, {8, 8, 8, 4}},
 };
 constexpr int kNumPlans = sizeof(kPlans) / sizeof(kPlans[0]);
 
-constexpr int plan_index(int n) {
+constexpr int plan_index(int n, int variant = 0) {
     for (int i = 0; i < kNumPlans; ++i)
-        if (kPlans[i].n == n) return i;
+        if (kPlans[i].n == n && kPlans[i].variant == variant) return i;
     return -1;
 }
 
 // Number of twiddle entries of a plan: every pass after the first holds
 // (R - 1) * Ns entries, entry [(r - 1) * Ns + j] = exp(-2 pi i j r / (Ns R)).
-constexpr int twiddle_count(int n) {
-    const int p = plan_index(n);
-    if (p < 0) return 0;
+constexpr int twiddle_count_key(int key) {
     int ns = 1, total = 0;
-    for (int k = 0; k < kPlans[p].npass; ++k) {
-        if (ns > 1) total += (kPlans[p].r[k] - 1) * ns;
-        ns *= kPlans[p].r[k];
+    for (int k = 0; k < kPlans[key].npass; ++k) {
+        if (ns > 1) total += (kPlans[key].r[k] - 1) * ns;
+        ns *= kPlans[key].r[k];
     }
     return total;
 }

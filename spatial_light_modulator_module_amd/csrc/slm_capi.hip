@@ -30,7 +30,7 @@ namespace {
 thread_local std::string g_err;
 int g_device = -1;
 std::mutex g_mu;
-std::map<std::tuple<int, int, int>, void*> g_twiddles;  // (device, n, precision) -> table
+std::map<std::tuple<int, int, int>, void*> g_twiddles;  // (device, plan key, precision) -> table
 ncclComm_t g_comm = nullptr;
 int g_comm_rank = 0, g_comm_size = 1;
 
@@ -73,20 +73,19 @@ int ensure_device() {
     return 0;
 }
 
-// Twiddle table of one transform length, in the pass order of kPlans:
-// entry [(r - 1) * Ns + j] = exp(-2 pi i j r / (Ns R)), computed in double and
+// Twiddle table of one radix plan, in its pass order: entry
+// [(r - 1) * Ns + j] = exp(-2 pi i j r / (Ns R)), computed in double and
 // stored as float2 (PREC_F32) or double2 (PREC_F64).
-int get_twiddles(int n, int prec, const void** out) {
+int get_twiddles(int pk, int prec, const void** out) {
     std::lock_guard<std::mutex> lk(g_mu);
-    auto key = std::make_tuple(g_device, n, prec);
+    auto key = std::make_tuple(g_device, pk, prec);
     auto it = g_twiddles.find(key);
     if (it != g_twiddles.end()) {
         *out = it->second;
         return 0;
     }
-    const int pi = plan_index(n);
-    if (pi < 0) return fail(SLM_ERR_UNSUPPORTED, "unsupported transform length %d", n);
-    const RadixPlan& pl = kPlans[pi];
+    if (pk < 0 || pk >= kNumPlans) return fail(SLM_ERR_UNSUPPORTED, "unknown plan key %d", pk);
+    const RadixPlan& pl = kPlans[pk];
     std::vector<double> host;  // interleaved re, im
     int ns = 1;
     for (int k = 0; k < pl.npass; ++k) {
@@ -179,6 +178,7 @@ int relayout(const V* in, V* out, long long n, int H, int W, bool to_blocked, hi
 struct slm_plan {
     int algo = 0, B = 0, H = 0, W = 0, tt = 1, has_ain = 0, max_loops = 0;
     int cw = 4, nwg = 0, col_threads = 0, row_threads = 0, rpw = 0;
+    int row_key = -1, col_key = -1;  // radix plans (kPlans) of the row / column transforms
     int device = 0;
     long long holo = 0;
     hipStream_t stream = nullptr;
@@ -214,15 +214,29 @@ namespace {
 // Column tile width. With the blocked state layout a 4-column panel is one
 // contiguous run, so the narrowest tile already moves whole lines and keeps
 // the most workgroups (and LDS headroom) per CU; SLM_COL_CW overrides.
-int pick_cw(int H, int W, int B) {
-    (void)B;
+int pick_cw(int ck, int W) {
     if (const char* s = std::getenv("SLM_COL_CW")) {
         const int cw = std::atoi(s);
-        if (col_fn(H, cw, COL_GS_MAIN, TGT_F32, PREC_F32) && W % cw == 0) return cw;
+        if (col_fn(ck, cw, COL_GS_MAIN, TGT_F32, PREC_F32) && W % cw == 0) return cw;
     }
     for (int cw : {4, 8, 16})
-        if (W % cw == 0 && col_fn(H, cw, COL_GS_MAIN, TGT_F32, PREC_F32)) return cw;
+        if (W % cw == 0 && col_fn(ck, cw, COL_GS_MAIN, TGT_F32, PREC_F32)) return cw;
     return 0;
+}
+
+// Radix plan of one axis: the narrow variant (half the elements per thread)
+// when the wide one would leave fewer than 4 waves per SIMD on the chip
+// (e.g. a single 1024^2 hologram), else the wide one. $SLM_PLAN=wide|narrow
+// forces a variant where it exists.
+int pick_plan(int n, long long elems) {
+    const int wide = plan_index(n, 0), narrow = plan_index(n, 1);
+    if (narrow < 0) return wide;
+    if (const char* s = std::getenv("SLM_PLAN")) {
+        if (!std::strcmp(s, "wide")) return wide;
+        if (!std::strcmp(s, "narrow")) return narrow;
+    }
+    const long long waves = elems / kPlans[wide].e / 64;
+    return waves < 4LL * 1024 ? narrow : wide;
 }
 
 int begin_launch(slm_plan* p, int cls) {
@@ -277,7 +291,7 @@ ColParams col_params(slm_plan* p) {
 }
 
 int launch_row(slm_plan* p, int mode, const RowParams& rp, int cls) {
-    RowFn fn = row_fn(p->W, mode, p->prec);
+    RowFn fn = row_fn(p->row_key, mode, p->prec);
     if (!fn) return fail(SLM_ERR_UNSUPPORTED, "no row kernel for width %d mode %d", p->W, mode);
     int rc = begin_launch(p, cls);
     if (rc) return rc;
@@ -288,7 +302,7 @@ int launch_row(slm_plan* p, int mode, const RowParams& rp, int cls) {
 
 int launch_col(slm_plan* p, int mode, const ColParams& cp, int cls) {
     const int tt = (mode == COL_EXPECTED || mode == COL_FFT_FWD || mode == COL_FFT_INV) ? TGT_F32 : p->tt;
-    ColFn fn = col_fn(p->H, p->cw, mode, tt, p->prec);
+    ColFn fn = col_fn(p->col_key, p->cw, mode, tt, p->prec);
     if (!fn) return fail(SLM_ERR_UNSUPPORTED, "no column kernel for height %d cw %d mode %d", p->H, p->cw, mode);
     int rc = begin_launch(p, cls);
     if (rc) return rc;
@@ -507,18 +521,20 @@ int slm_plan_create(int algo, int batch, int height, int width, int tgt_type, in
     p->max_loops = max_loops;
     p->device = g_device;
     p->holo = (long long)height * width;
-    p->cw = pick_cw(height, width, batch);
+    p->row_key = pick_plan(width, (long long)batch * p->holo);
+    p->col_key = pick_plan(height, (long long)batch * p->holo);
+    p->cw = pick_cw(p->col_key, width);
     if (!p->cw) {
         delete p;
         return fail(SLM_ERR_UNSUPPORTED, "no column tiling for %dx%d", height, width);
     }
     p->nwg = width / p->cw;
-    p->col_threads = col_threads(height, p->cw);
-    p->row_threads = row_threads(width);
-    p->rpw = row_rpw(width);
+    p->col_threads = col_threads(p->col_key, p->cw);
+    p->row_threads = row_threads(p->row_key);
+    p->rpw = row_rpw(p->row_key);
     if (const char* e = std::getenv("SLM_PRECISION")) p->prec = (std::strcmp(e, "f32") == 0) ? PREC_F32 : PREC_F64;
-    int rc = get_twiddles(width, p->prec, &p->tw_row);
-    if (!rc) rc = get_twiddles(height, p->prec, &p->tw_col);
+    int rc = get_twiddles(p->row_key, p->prec, &p->tw_row);
+    if (!rc) rc = get_twiddles(p->col_key, p->prec, &p->tw_col);
     if (rc) {
         delete p;
         return rc;
@@ -595,8 +611,8 @@ int slm_plan_set_precision(slm_plan* p, int precision) {
         return fail(SLM_ERR_ARG, "unknown precision %d", precision);
     HIP_TRY(hipSetDevice(p->device));
     const void *tr = nullptr, *tc = nullptr;
-    RC(get_twiddles(p->W, precision, &tr));
-    RC(get_twiddles(p->H, precision, &tc));
+    RC(get_twiddles(p->row_key, precision, &tr));
+    RC(get_twiddles(p->col_key, precision, &tc));
     p->prec = precision;
     p->tw_row = tr;
     p->tw_col = tc;
@@ -609,7 +625,11 @@ int slm_plan_set_ain(slm_plan* p, const float* ain) {
     if (!p || !ain) return fail(SLM_ERR_ARG, "null argument");
     if (!p->has_ain) return fail(SLM_ERR_STATE, "plan was created without an incoming amplitude");
     HIP_TRY(hipSetDevice(p->device));
-    HIP_TRY(hipMemcpy(p->ain, ain, (size_t)p->holo * sizeof(float), hipMemcpyHostToDevice));
+    // Uploads go on the plan stream: the plan's non-blocking stream is not
+    // ordered after null-stream copies, and a pageable hipMemcpy may return
+    // before its DMA has landed.
+    HIP_TRY(hipMemcpyAsync(p->ain, ain, (size_t)p->holo * sizeof(float), hipMemcpyHostToDevice, p->stream));
+    HIP_TRY(hipStreamSynchronize(p->stream));
     return 0;
 }
 
@@ -623,7 +643,8 @@ int slm_plan_set_phase(slm_plan* p, const float* phase) {
     }
     const size_t bytes = (size_t)p->B * p->holo * sizeof(float);
     if (!p->phase_in) HIP_TRY(hipMalloc((void**)&p->phase_in, bytes));
-    HIP_TRY(hipMemcpy(p->phase_in, phase, bytes, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpyAsync(p->phase_in, phase, bytes, hipMemcpyHostToDevice, p->stream));
+    HIP_TRY(hipStreamSynchronize(p->stream));
     p->phase_set = true;
     return 0;
 }
@@ -648,7 +669,8 @@ int slm_plan_set_lr(slm_plan* p, const float* lr) {
     if (!p || !lr) return fail(SLM_ERR_ARG, "null argument");
     if (p->algo != SLM_ALGO_GD) return fail(SLM_ERR_STATE, "learning rates apply to GD plans");
     HIP_TRY(hipSetDevice(p->device));
-    HIP_TRY(hipMemcpy(p->lr, lr, (size_t)p->max_loops * sizeof(float), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpyAsync(p->lr, lr, (size_t)p->max_loops * sizeof(float), hipMemcpyHostToDevice, p->stream));
+    HIP_TRY(hipStreamSynchronize(p->stream));
     p->lr_set = true;
     return 0;
 }
@@ -735,6 +757,9 @@ int slm_plan_info(slm_plan* p, int* info) {
     info[2] = p->col_threads;
     info[3] = p->row_threads;
     info[4] = p->rpw;
+    info[5] = p->row_key;
+    info[6] = p->col_key;
+    info[7] = p->prec;
     return 0;
 }
 

@@ -31,3 +31,17 @@ def test_fft2_roundtrip_large(gpu):
     y = gpu.fft2(gpu.fft2(x), inverse=True) / (4096 * 4096)
     err = np.linalg.norm(y - x) / np.linalg.norm(x)
     assert err < 2e-6, f"round trip error {err:.3e}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["wide", "narrow"])
+@pytest.mark.parametrize("shape", [(256, 512), (768, 1024), (1024, 2048)])
+def test_fft2_plan_variants(gpu, monkeypatch, variant, shape):
+    """Both radix-plan variants (wide: 16-24 elements per thread; narrow: half)
+    compute the same transform."""
+    monkeypatch.setenv("SLM_PLAN", variant)
+    rng = np.random.default_rng(3)
+    x = (rng.standard_normal(shape) + 1j * rng.standard_normal(shape)).astype(np.complex64)
+    got = gpu.fft2(x).astype(np.complex128)
+    ref = np.fft.fft2(x.astype(np.complex128))
+    assert np.linalg.norm(got - ref) / np.linalg.norm(ref) < 2e-6
