@@ -32,7 +32,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# load libslm_hip.so (and with it the system HIP runtime) before torch
+# libslm_hip.so (torch is imported ahead of it: one HIP runtime per process)
 from spatial_light_modulator_module_amd import _lib  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
@@ -210,7 +210,8 @@ def main():
             _lib.comm_destroy()
         return
 
-    key = f"gs_{n}x{n}_b{bper}_it{iters}_f32"
+    prec = info["precision"]  # butterflies / twiddles / exchanges; HBM state is complex64
+    key = f"gs_{n}x{n}_b{bper}_it{iters}_{prec}"
     traffic = pmc_traffic(key)
     dr = rows[dom]
     roofline = {"bound": "hbm", "achieved": round(dr["achieved_gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -222,13 +223,13 @@ def main():
     out = {
         "metric": METRIC, "value": round(value, 3), "unit": "holograms/s", "n_gpus": d.world,
         "steps": opt.steps, "warmup": opt.warmup, "ms_per_step": round(ms_per_step, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": prec,
         "data": "synthetic (uniform[0,255) float32 targets, default_rng(1234+b))",
         "config": {"workload": f"GS {n}x{n}, {iters} iterations, {bper} hologram(s) per GPU, float32 target, "
                                "uniform incoming intensity, tolerance 0 (BASELINE.json configs[1])",
                    "height": n, "width": n, "iters": iters, "batch_per_gpu": bper, "global_batch": bper * d.world,
                    "parallelism": f"dp{d.world} (independent holograms; RCCL gather of phases to rank 0)",
-                   "col_tile": info},
+                   "storage": "complex64 field, float32 target/phase", "col_tile": info},
         "gs_iter_ms": round(ms_per_step / iters, 5),
         "roofline": roofline,
         "check": "ok" if ok else "FAILED",

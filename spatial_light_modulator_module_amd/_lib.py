@@ -78,6 +78,26 @@ _SIGNATURES = [
 _lib = None
 
 
+def _bind_one_hip_runtime():
+    """Keep a single HIP/HSA/RCCL runtime per process.
+
+    PyTorch-ROCm ships its own libamdhip64 / libhsa-runtime64 / librccl under
+    unversioned file names, so a process that loads the system copies (through
+    this library) and then imports torch maps two HIP and two HSA runtimes and
+    aborts in their exit-time destructors. Importing torch first makes this
+    library's NEEDED sonames (libamdhip64.so.7, librccl.so.1) resolve to the
+    copies already mapped. torch is only plumbing here (torch.distributed for
+    multi-process control); SLM_SYSTEM_HIP=1 skips it for torch-free processes
+    that want the system ROCm runtime (they must then never import torch).
+    """
+    if os.environ.get("SLM_SYSTEM_HIP", "0") == "1":
+        return
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def load() -> ctypes.CDLL:
     """Load libslm_hip.so once; raise ImportError if it was never built."""
     global _lib
@@ -88,6 +108,7 @@ def load() -> ctypes.CDLL:
             f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "(or `make -C spatial_light_modulator_module_amd/csrc`). There is no CPU fallback."
         )
+    _bind_one_hip_runtime()
     lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
     for name, res, args in _SIGNATURES:
         fn = getattr(lib, name)

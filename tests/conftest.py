@@ -1,7 +1,7 @@
 """Shared pytest configuration.
 
-The HIP library is loaded before anything imports torch so that one HIP
-runtime (the system ROCm one libslm_hip.so links) serves the whole process.
+The package is imported first: loading libslm_hip.so imports torch ahead of
+it (_lib._bind_one_hip_runtime) so the whole process shares one HIP runtime.
 """
 import os
 import sys

@@ -1,0 +1,139 @@
+"""The N > 1 path on CPU: world_size-2 gloo process groups.
+
+Holograms are independent: ranks take contiguous shards
+(parallel.shard_range), compute with no data-path collective, and only the
+results travel (RCCL send/recv to rank 0 on the GPU box; gloo here). The HIP
+compute is replaced by the float64 oracle in these CPU tests - the sharding,
+gather order, file output and the reference CLI behaviour are what is tested.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from oracle import gs_gd_oracle as orc
+from spatial_light_modulator_module_amd import parallel
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def oracle_run_gs(targets, loops, tol=0.0, ain=None, initial_phase=None):
+    """Stand-in with run_gs's return contract, computed by the oracle."""
+    phases, es, errs = [], [], []
+    for t in targets:
+        ph, exp, err = orc.gerchberg_saxton_faithful(t, loops, tol)
+        phases.append(ph.astype(np.float32))
+        es.append(exp)
+        errs.append(list(err))
+    b = len(targets)
+    return np.stack(phases), np.stack(es), errs, np.ones(b), np.ones(b)
+
+
+@pytest.mark.parametrize("total,nranks", [(0, 2), (1, 2), (5, 2), (7, 3), (8, 8), (3, 5)])
+def test_shards_cover_the_batch(total, nranks):
+    seen = []
+    for r in range(nranks):
+        seen += list(parallel.shard_range(total, nranks, r))
+    assert seen == list(range(total))
+    counts = parallel.shard_counts(total, nranks)
+    assert max(counts) - min(counts) <= 1 and sum(counts) == total
+
+
+def test_assemble_checks_counts():
+    parts = [np.zeros((2, 4, 4)), np.ones((1, 4, 4))]
+    out = parallel.assemble(parts, [2, 1])
+    assert out.shape == (3, 4, 4) and out[2].min() == 1
+    with pytest.raises(ValueError):
+        parallel.assemble(parts, [1, 2])
+
+
+def _setup(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    return dist
+
+
+def _batch_worker(rank, world, port, targets, loops, out_path):
+    dist = _setup(rank, world, port)
+    mine = parallel.shard_range(len(targets), world, rank)
+    phase, _, _, _, _ = oracle_run_gs(targets[mine.start:mine.stop], loops)
+    parts = [None] * world
+    dist.all_gather_object(parts, phase)
+    if rank == 0:
+        full = parallel.assemble(parts, parallel.shard_counts(len(targets), world))
+        np.save(out_path, full)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_batch_equals_single_process(tmp_path):
+    rng = np.random.default_rng(3)
+    targets = rng.integers(0, 256, size=(5, 64, 64)).astype(np.uint8)
+    out = str(tmp_path / "phase.npy")
+    mp.spawn(_batch_worker, args=(2, _free_port(), targets, 4, out), nprocs=2, join=True)
+    want, _, _, _, _ = oracle_run_gs(targets, 4)
+    np.testing.assert_array_equal(np.load(out), want)
+
+
+def _make_sequence(root, n):
+    from PIL import Image
+
+    d = os.path.join(root, "images", "moving_traps", "seq")
+    os.makedirs(d)
+    rng = np.random.default_rng(11)
+    for i in range(n):
+        img = np.zeros((64, 128), np.uint8)
+        y, x = rng.integers(4, 60), rng.integers(4, 124)
+        img[y - 2:y + 2, x - 2:x + 2] = 255
+        Image.fromarray(img).save(os.path.join(d, f"{i}.png"))
+
+
+def _sequence_worker(rank, world, port, root):
+    _setup(rank, world, port)
+    from spatial_light_modulator_module_amd import generate_hologram_sequence as ghs
+
+    os.chdir(root)
+    ghs.run_gs = oracle_run_gs  # CPU stand-in for the GPU batch
+    errors = ghs.cli(["seq", "-v", "w2", "-ct2pi", "255", "-loops", "3", "-p"], plot=False)
+    np.save(os.path.join(root, f"errors_rank{rank}.npy"), np.array([errors[i] for i in sorted(errors)]))
+    import torch.distributed as dist
+
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sequence_cli_two_ranks_matches_single(tmp_path, monkeypatch):
+    from spatial_light_modulator_module_amd import generate_hologram_sequence as ghs
+
+    n = 5
+    two, one = tmp_path / "two", tmp_path / "one"
+    for r in (two, one):
+        r.mkdir()
+        _make_sequence(str(r), n)
+    mp.spawn(_sequence_worker, args=(2, _free_port(), str(two)), nprocs=2, join=True)
+
+    monkeypatch.chdir(one)
+    monkeypatch.setattr(ghs, "run_gs", oracle_run_gs)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    errors = ghs.cli(["seq", "-v", "w2", "-ct2pi", "255", "-loops", "3", "-p"], plot=False)
+    assert sorted(errors) == list(range(n))
+    for i in range(n):
+        a = np.load(two / "holograms" / "seq_w2_holograms" / f"{i}.npy")
+        b = np.load(one / "holograms" / "seq_w2_holograms" / f"{i}.npy")
+        assert a.dtype == np.float64 and a.shape == (64, 128)
+        np.testing.assert_array_equal(a, b)
+        assert (two / "images" / "moving_traps" / "seq_w2_preview" / f"{i}.png").exists()
+    # both ranks see the gathered error evolutions of every frame
+    for r in (0, 1):
+        np.testing.assert_array_equal(np.load(two / f"errors_rank{r}.npy"),
+                                      np.array([errors[i] for i in range(n)]))

@@ -1,0 +1,162 @@
+"""Host-side logic of the drop-in CLI and API (no GPU): argument defaults,
+hologram names, deflect / lens post-processing against the reference's
+per-pixel loops (src/generate_hologram.py:178-203,
+src/wavefront_correction.py:440-449), and the reference's error behaviour."""
+import argparse
+import os
+
+import numpy as np
+import pytest
+
+from oracle import gs_gd_oracle as orc
+from spatial_light_modulator_module_amd import algorithms as alg
+from spatial_light_modulator_module_amd import constants as c
+from spatial_light_modulator_module_amd import generate_hologram as gh
+from spatial_light_modulator_module_amd import generate_hologram_sequence as ghs
+
+
+def test_parser_defaults_match_reference():
+    a = gh.build_parser().parse_args(["x.png"])
+    assert (a.incomming_intensity, a.initial_guess, a.destination_directory) == ("uniform", "random", "holograms")
+    assert (a.algorithm, a.tolerance, a.max_loops, a.learning_rate) == ("gerchberg_saxton", 0, 42, 0.005)
+    assert (a.white_attention, a.unsettle, a.gif_type, a.gif_skip) == (1, 0, "i", 1)
+    assert a.deflect is None and a.lens is None and not a.quarterize and not a.invert
+    s = ghs.build_parser().parse_args(["traps", "-v", "1", "-ct2pi", "255"])
+    assert (s.max_loops, s.tolerance, s.incomming_intensity, s.preview) == (5, 0, "uniform", False)
+    with pytest.raises(SystemExit):
+        ghs.build_parser().parse_args(["traps"])  # -ct2pi is required
+
+
+def test_hologram_name_keeps_reference_whitespace():
+    a = gh.build_parser().parse_args(["cat.png", "-alg", "gradient_descent", "-q", "-i", "-deflect", "1", "2",
+                                      "-lens", "0.5"])
+    sep = " " * 8
+    # argparse leaves non-string defaults untyped: -wa defaults to the int 1, hence "mr1"
+    expected = ("cat_quarter_inverted" + sep + "_gradient_descent" + sep + "_lr0.005_mr1_unsettle0" + sep
+                + "_loops42" + sep + "_deflect_x1.0_y2.0_lens0.5")
+    assert gh.make_hologram_name(a, "cat") == expected
+    b = gh.build_parser().parse_args(["-deflect", "1", "1"])
+    assert gh.make_hologram_name(b, "analytical") == "analytical_deflect_x1.0_y1.0"
+
+
+def _deflect_loop_rows(angle, rows):
+    x_angle, y_angle = angle
+    const = 2 * np.pi * c.px_distance / c.wavelength
+    out = np.zeros((len(rows), c.slm_width))
+    for r, i in enumerate(rows):
+        for j in range(c.slm_width):
+            new_phase = const * (np.sin(y_angle * c.u) * i + np.sin(x_angle * c.u) * j)
+            out[r, j] = new_phase % (2 * np.pi)
+    return out
+
+
+@pytest.mark.parametrize("angle", [(1.0, 1.0), (-2.5, 0.75)])
+def test_deflect_is_bitwise_the_reference_loop(angle):
+    rows = list(range(0, c.slm_height, 97)) + [c.slm_height - 1]
+    got = gh.deflect_2pi(angle)
+    assert got.shape == (c.slm_height, c.slm_width) and got.dtype == np.float64
+    np.testing.assert_array_equal(got[rows], _deflect_loop_rows(angle, rows))
+
+
+def _lens_loop(focal_length, shape):
+    h, w = shape
+    out = np.zeros((h, w), dtype=np.uint8)
+    for i in range(h):
+        for j in range(w):
+            r = c.px_distance * np.sqrt((i - h / 2) ** 2 + (j - w / 2) ** 2)
+            ps = 2 * np.pi * focal_length / c.wavelength * (1 - np.sqrt(1 + r**2 / focal_length**2))
+            out[i, j] = ps % (2 * np.pi)
+    return out
+
+
+@pytest.mark.parametrize("f", [0.5, -1.2, 3.0])
+def test_lens_is_bitwise_the_reference_loop(f):
+    np.testing.assert_array_equal(gh.lens(f, (48, 64)), _lens_loop(f, (48, 64)))
+
+
+def test_analytical_hologram_cli(tmp_path, monkeypatch):
+    monkeypatch.chdir(tmp_path)
+    path = gh.cli(["-deflect", "1", "0.5", "-lens", "2.0", "-dest_dir", "out"])
+    assert os.path.basename(path) == "analytical_deflect_x1.0_y0.5_lens2.0.npy"
+    h = np.load(path)
+    want = gh.add_lens(gh.deflect_hologram(np.zeros((c.slm_height, c.slm_width)), (1.0, 0.5)), 2.0)
+    np.testing.assert_array_equal(h, want)
+    # a second run does not overwrite: originalize_name appends _1
+    path2 = gh.cli(["-deflect", "1", "0.5", "-lens", "2.0", "-dest_dir", "out"])
+    assert path2.endswith("analytical_deflect_x1.0_y0.5_lens2.0_1.npy")
+
+
+def test_prepare_target_shape_and_padding(tmp_path, monkeypatch):
+    from PIL import Image
+
+    monkeypatch.chdir(tmp_path)
+    os.makedirs("images")
+    img = np.zeros((100, 200), np.uint8)
+    img[:, :] = 200
+    Image.fromarray(img).save("images/wide.png")
+    a = gh.build_parser().parse_args(["wide.png"])
+    t = gh.prepare_target("wide.png", a)
+    assert t.shape == (c.slm_height, c.slm_width) and t.dtype == np.uint8
+    assert t[0, 512] == 0 and t[384, 512] == 200  # black bands from pad_to_square
+    a.invert = True
+    assert gh.prepare_target("wide.png", a)[384, 512] == 55
+    a.invert, a.quarterize = False, True
+    q = gh.prepare_target("wide.png", a)
+    assert q[700, 1000] == 0 and q[192, 256] == 200
+
+
+def _args(**kw):
+    base = dict(incomming_intensity="uniform", tolerance=0.0, max_loops=5, gif=False, print_info=False,
+                plot_error=False, learning_rate=0.005, white_attention=1.0, unsettle=0, initial_guess="random",
+                random_seed=42)
+    base.update(kw)
+    return argparse.Namespace(**base)
+
+
+def test_zero_loops_raise_like_the_reference():
+    t = np.ones((64, 64), np.uint8)
+    with pytest.raises(UnboundLocalError):
+        alg.gerchberg_saxton(t, _args(max_loops=0))
+    with pytest.raises(UnboundLocalError):
+        alg.gradient_descent(t.astype(np.float64), _args(max_loops=0))
+    with pytest.raises(UnboundLocalError):  # error = tol + 1 is not > tol for huge tol
+        alg.gerchberg_saxton(t, _args(tolerance=1e17))
+
+
+def test_gd_argument_errors():
+    t = np.ones((64, 64))
+    with pytest.raises(ValueError):
+        alg.gradient_descent(t, _args(initial_guess="banana"))
+    with pytest.raises(ZeroDivisionError):
+        alg.gradient_descent(t, _args(max_loops=1, unsettle=5))
+
+
+def test_unsupported_shape_is_rejected():
+    with pytest.raises(ValueError):
+        alg.gerchberg_saxton(np.ones((100, 64)), _args())
+
+
+@pytest.mark.parametrize("loops,unsettle", [(10, 0), (10, 1), (12, 3), (7, 2), (100, 4)])
+def test_learning_rate_schedule_matches_oracle(loops, unsettle):
+    rates, after = alg.learning_rates(0.01, loops, unsettle)
+    for n in (1, loops // 2, loops):
+        want, final = orc.unsettle_schedule(0.01, loops, unsettle, n)
+        np.testing.assert_array_equal(rates[:n], want)
+        assert after[n] == final
+
+
+def test_initial_guess_matches_oracle():
+    t = np.ones((64, 128))
+    amp = np.ones(t.shape)
+    for kind in ("random", "old", "unnormed", "zeros", "ones"):
+        np.testing.assert_array_equal(alg.make_initial_guess(kind, amp, t, 7),
+                                      orc.make_initial_guess(kind, amp, t, 7))
+    assert alg.make_initial_guess("fourier", amp, t, 7) is None
+
+
+def test_target_dtype_rules():
+    _, tt = alg.target_for_device(np.zeros((64, 64), np.uint8))
+    assert tt == alg.TGT_U8
+    for dt in (np.float64, np.float32, np.int32, np.uint16):
+        t, tt = alg.target_for_device(np.zeros((64, 64), dt))
+        assert tt == alg.TGT_F32 and t.dtype == np.float32
