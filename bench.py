@@ -49,7 +49,7 @@ def parse():
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the 4096^2 / batched secondary measurements")
-    ap.add_argument("--cpu-sample-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-sample-seconds", type=float, default=20.0)
     return ap.parse_args()
 
 
@@ -141,6 +141,19 @@ def cpu_baseline(n: int, iters: int, budget_s: float):
             "sample": f"{k} GS iterations of the NumPy/SciPy float64 restatement (oracle/gs_gd_oracle.py) on one "
                       f"{n}x{n} float32 target in {dt:.1f} s, extrapolated to {iters} iterations per hologram",
             "ms_per_iter": per_iter * 1e3, "host_cpus": os.cpu_count()}
+
+
+def pcie_inclusive(plan, host_targets, iters, reps=5):
+    """The drop-in boundary's host-to-host rate: target upload, the run and the
+    phase download per step (never the headline value)."""
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        plan.set_target(host_targets)
+        plan.run(iters)
+        plan.read(phase=True, expected=False, stats=False, iters=False)
+    wall = (time.perf_counter() - t0) / reps
+    return {"holograms_per_s": host_targets.shape[0] / wall, "ms_per_step": wall * 1e3,
+            "includes": "target upload + relayout, run, phase download (pageable host memory)"}
 
 
 def secondary(n, batch, iters):
@@ -235,7 +248,7 @@ def main():
         "check": "ok" if ok else "FAILED",
     }
     if d.world == 1 and not opt.no_extra:
-        extra = {}
+        extra = {"pcie_inclusive": pcie_inclusive(plan, targets(0, bper, n), iters)}
         try:
             extra["gs_4096"] = secondary(4096, 1, 20)
             extra["gs_1024_batch64"] = secondary(1024, 64, 20)

@@ -2,6 +2,7 @@
 // sequencing of the fused GS / GD iterations, HIP-event timing, and the
 // RCCL gather of phases for one-process-per-GPU runs. C-ABI in
 // include/slm_hip.h.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -239,23 +240,28 @@ int pick_plan(int n, long long elems) {
     return waves < 4LL * 1024 ? narrow : wide;
 }
 
-int begin_launch(slm_plan* p, int cls) {
-    if (!p->timing) return 0;
-    if (p->ev_used == p->ev_pool.size()) {
-        hipEvent_t a, b;
-        HIP_TRY(hipEventCreate(&a));
-        HIP_TRY(hipEventCreate(&b));
-        p->ev_pool.emplace_back(a, b);
-        p->ev_class.push_back(cls);
+// Every kernel of a run is launched through here. In a timed run
+// (slm_plan_run_timed) each launch carries its own start/stop events
+// (hipExtLaunchKernelGGL): the dispatch packet stamps them, so they bracket the
+// kernel's execution alone, as rocprofv3's kernel trace does, with no marker
+// packets between kernels.
+template <typename F, typename... Args>
+int launch(slm_plan* p, int cls, F fn, dim3 grid, dim3 block, Args... args) {
+    if (p->timing) {
+        if (p->ev_used == p->ev_pool.size()) {
+            hipEvent_t a, b;
+            HIP_TRY(hipEventCreate(&a));
+            HIP_TRY(hipEventCreate(&b));
+            p->ev_pool.emplace_back(a, b);
+            p->ev_class.push_back(cls);
+        }
+        p->ev_class[p->ev_used] = cls;
+        auto& ev = p->ev_pool[p->ev_used++];
+        hipExtLaunchKernelGGL(fn, grid, block, 0, p->stream, ev.first, ev.second, 0, args...);
+    } else {
+        hipLaunchKernelGGL(fn, grid, block, 0, p->stream, args...);
     }
-    p->ev_class[p->ev_used] = cls;
-    HIP_TRY(hipEventRecord(p->ev_pool[p->ev_used].first, p->stream));
-    return 0;
-}
-int end_launch(slm_plan* p) {
-    if (!p->timing) return 0;
-    HIP_TRY(hipEventRecord(p->ev_pool[p->ev_used].second, p->stream));
-    ++p->ev_used;
+    HIP_TRY(hipGetLastError());
     return 0;
 }
 
@@ -293,22 +299,14 @@ ColParams col_params(slm_plan* p) {
 int launch_row(slm_plan* p, int mode, const RowParams& rp, int cls) {
     RowFn fn = row_fn(p->row_key, mode, p->prec);
     if (!fn) return fail(SLM_ERR_UNSUPPORTED, "no row kernel for width %d mode %d", p->W, mode);
-    int rc = begin_launch(p, cls);
-    if (rc) return rc;
-    hipLaunchKernelGGL(fn, dim3(p->H / p->rpw, p->B), dim3(p->row_threads), 0, p->stream, rp);
-    HIP_TRY(hipGetLastError());
-    return end_launch(p);
+    return launch(p, cls, fn, dim3(p->H / p->rpw, p->B), dim3(p->row_threads), rp);
 }
 
 int launch_col(slm_plan* p, int mode, const ColParams& cp, int cls) {
     const int tt = (mode == COL_EXPECTED || mode == COL_FFT_FWD || mode == COL_FFT_INV) ? TGT_F32 : p->tt;
     ColFn fn = col_fn(p->col_key, p->cw, mode, tt, p->prec);
     if (!fn) return fail(SLM_ERR_UNSUPPORTED, "no column kernel for height %d cw %d mode %d", p->H, p->cw, mode);
-    int rc = begin_launch(p, cls);
-    if (rc) return rc;
-    hipLaunchKernelGGL(fn, dim3(p->nwg, p->B), dim3(p->col_threads), 0, p->stream, cp);
-    HIP_TRY(hipGetLastError());
-    return end_launch(p);
+    return launch(p, cls, fn, dim3(p->nwg, p->B), dim3(p->col_threads), cp);
 }
 
 StatsParams stats_params(slm_plan* p, double tol) {
@@ -328,11 +326,7 @@ StatsParams stats_params(slm_plan* p, double tol) {
 int launch_finalize(slm_plan* p, double tol, int iter) {
     StatsParams s = stats_params(p, tol);
     s.iter = iter;
-    int rc = begin_launch(p, SLM_KERNEL_OTHER);
-    if (rc) return rc;
-    hipLaunchKernelGGL(stats_finalize_kernel, dim3(p->B), dim3(256), 0, p->stream, s);
-    HIP_TRY(hipGetLastError());
-    return end_launch(p);
+    return launch(p, SLM_KERNEL_OTHER, stats_finalize_kernel, dim3(p->B), dim3(256), s);
 }
 
 #define RC(x)                 \
@@ -412,14 +406,10 @@ int enqueue_gd(slm_plan* p, int loops, double tol, int checked, float wa) {
         RC(launch_row(p, ROW_GD_MAIN, rp, SLM_KERNEL_ROW_MAIN));
     }
     {
-        int rc = begin_launch(p, SLM_KERNEL_OTHER);
-        if (rc) return rc;
         const long long n = (long long)p->B * p->holo;
         const int grid = (int)std::min<long long>(4096, (n + 255) / 256);
-        hipLaunchKernelGGL(field_phase_kernel, dim3(grid), dim3(256), 0, p->stream, (const float2*)p->field,
-                           p->phase_out, n, p->H, p->W);
-        HIP_TRY(hipGetLastError());
-        RC(end_launch(p));
+        RC(launch(p, SLM_KERNEL_OTHER, field_phase_kernel, dim3(grid), dim3(256), (const float2*)p->field,
+                  p->phase_out, n, p->H, p->W));
     }
     cp.in = p->xa;
     cp.in_alt = p->xb;
@@ -434,20 +424,11 @@ int enqueue_run(slm_plan* p, int loops, double tol, int checked, float wa) {
         return fail(SLM_ERR_ARG, "loops %d outside [1, %d]", loops, p->max_loops);
     if (p->algo == SLM_ALGO_GD && !p->lr_set) return fail(SLM_ERR_STATE, "learning rates not set");
     HIP_TRY(hipSetDevice(p->device));
-    {
-        int rc = begin_launch(p, SLM_KERNEL_OTHER);
-        if (rc) return rc;
-        hipLaunchKernelGGL(fill_int_kernel, dim3((p->B + 255) / 256), dim3(256), 0, p->stream, p->stop, p->B,
-                           INT_MAX);
-        HIP_TRY(hipGetLastError());
-        RC(end_launch(p));
-    }
+    RC(launch(p, SLM_KERNEL_OTHER, fill_int_kernel, dim3((p->B + 255) / 256), dim3(256), p->stop, p->B,
+              (int)INT_MAX));
     RC(p->algo == SLM_ALGO_GS ? enqueue_gs(p, loops, tol, checked) : enqueue_gd(p, loops, tol, checked, wa));
     StatsParams s = stats_params(p, tol);
-    RC(begin_launch(p, SLM_KERNEL_OTHER));
-    hipLaunchKernelGGL(stats_reduce_kernel, dim3(loops, p->B), dim3(256), 0, p->stream, s);
-    HIP_TRY(hipGetLastError());
-    RC(end_launch(p));
+    RC(launch(p, SLM_KERNEL_OTHER, stats_reduce_kernel, dim3(loops, p->B), dim3(256), s));
     return 0;
 }
 

@@ -18,7 +18,7 @@ import sys
 import numpy as np
 
 from . import parallel
-from .algorithms import _check_shape, _print_loops, expected_from, incoming_amplitude, run_gs
+from .algorithms import _check_shape, _print_loops, expected_from, hologram_from, incoming_amplitude, run_gs
 
 SEQ_BATCH = int(os.environ.get("SLM_SEQ_BATCH", "64"))  # frames per GPU launch batch
 
@@ -69,7 +69,7 @@ def generate_hologram_sequence(args, rank=None, nranks=None):
             sys.stdout.write(f"\rcreating {i}. hologram ")
             _print_loops(len(errs[k]), args.max_loops)
             errors[i] = errs[k]
-            np.save(f"{dest_dir_holograms}/{i}.npy", phase[k].astype(np.float64))
+            np.save(f"{dest_dir_holograms}/{i}.npy", hologram_from(phase[k]))
             if args.preview:
                 expected = expected_from(e[k], norm[k], emax[k])
                 Image.fromarray(expected).convert("L").save(f"{dest_dir_preview}/{i}.png")
