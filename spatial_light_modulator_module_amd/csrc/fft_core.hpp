@@ -335,6 +335,7 @@ template <int N, class C>
 struct Twiddles<N, C, TW_CACHED> {
     static constexpr int COUNT = TwCountOf<N, RadicesOf<N>>::value > 0 ? TwCountOf<N, RadicesOf<N>>::value : 1;
     C w[COUNT];
+    __device__ __forceinline__ void launder() {}
     template <int TwOff, int RegOff, int PowOff, int R, int Ns, bool INV>
     __device__ __forceinline__ void apply(C* u, int k, int) const {
         static_for<R - 1>([&](auto rc) {
@@ -346,12 +347,26 @@ struct Twiddles<N, C, TW_CACHED> {
 };
 template <int N, class C>
 struct Twiddles<N, C, TW_DIRECT> {
-    const C* __restrict__ table;
+    struct alignas(2 * sizeof(Scalar<C>)) Pod {  // trivially copyable twin of C
+        Scalar<C> x, y;
+    };
+    using GlobalPtr = const __attribute__((address_space(1))) Pod*;  // keeps global_load (not flat)
+    GlobalPtr table;
+    // The table is read-only, so the compiler may legally reuse the first
+    // transform's twiddle loads in the second one and keep them all live in
+    // between (dozens of float64 registers -> spills). Passing the pointer
+    // through an empty asm before each transform makes the loads distinct.
+    __device__ __forceinline__ void launder() {
+        unsigned long long q = (unsigned long long)table;
+        asm volatile("" : "+s"(q));
+        table = (GlobalPtr)q;
+    }
     template <int TwOff, int RegOff, int PowOff, int R, int Ns, bool INV>
     __device__ __forceinline__ void apply(C* u, int, int j) const {
         static_for<R - 1>([&](auto rc) {
             constexpr int r = decltype(rc)::value + 1;
-            const C t = table[TwOff + (r - 1) * Ns + j];
+            const int i = TwOff + (r - 1) * Ns + j;
+            const C t = mk<C>(table[i].x, table[i].y);
             u[r] = INV ? cmulc(u[r], t) : cmul(u[r], t);
         });
     }
@@ -360,6 +375,7 @@ template <int N, class C>
 struct Twiddles<N, C, TW_POWERS> {
     static constexpr int COUNT = TwPowCountOf<N, RadicesOf<N>>::value > 0 ? TwPowCountOf<N, RadicesOf<N>>::value : 1;
     C w1[COUNT];
+    __device__ __forceinline__ void launder() {}
     template <int TwOff, int RegOff, int PowOff, int R, int Ns, bool INV>
     __device__ __forceinline__ void apply(C* u, int k, int) const {
         C w[R];
@@ -404,7 +420,7 @@ __device__ __forceinline__ void load_twiddles_impl(Twiddles<N, C, MODE>& tw, int
 template <int N, class C, int MODE>
 __device__ __forceinline__ void load_twiddles(Twiddles<N, C, MODE>& tw, int t, const void* table) {
     if constexpr (MODE == TW_DIRECT)
-        tw.table = static_cast<const C*>(table);
+        tw.table = (typename Twiddles<N, C, MODE>::GlobalPtr)table;
     else
         load_twiddles_impl<N, C, MODE>(tw, t, static_cast<const C*>(table), RadicesOf<N>{});
 }
@@ -423,12 +439,36 @@ __device__ __forceinline__ void exchange_barrier() {
 }
 
 // ------------------------------------------------------------------------
-// Stockham driver. v[m] holds element t + T m on entry and the transform's
-// element t + T m on exit.
+// Stockham driver.
+//
+// State: v[m] holds element t + T m of the line between passes, as V. V is
+// complex64 whenever the LDS exchange is complex64 (the exchange rounds there
+// anyway), which halves the registers a float64 transform keeps live; each
+// butterfly widens its R inputs to the compute type C, and only the R values
+// of one butterfly group are ever live in C.
+//
+// The last pass hands each butterfly group k (slots k + r NB, r < R) to a
+// sink while it is still in C. Sinks either write it back to v, or apply an
+// element-wise epilogue and — when the next transform's first radix equals
+// this transform's last one, so that group k is the next first-pass group —
+// run that first pass in registers too (fft_pair): the projection between an
+// inverse and a forward transform then never rounds to complex64.
 // ------------------------------------------------------------------------
-template <int N, int E, bool INV, int Ns, int TwOff, int RegOff, int PowOff, class C, class Lds, class Tw, int R,
-          int... Rest>
-__device__ __forceinline__ void stockham_pass(C (&v)[E], int t, const Tw& tw, const Lds& lds) {
+#ifndef SLM_FUSE_PAIR
+#define SLM_FUSE_PAIR 1
+#endif
+#ifndef SLM_GROUP_FENCE
+#define SLM_GROUP_FENCE 1
+#endif
+
+template <class To, class From>
+__device__ __forceinline__ To cv(From a) {
+    return mk<To>((Scalar<To>)a.x, (Scalar<To>)a.y);
+}
+
+template <int N, int E, bool INV, int Ns, int TwOff, int RegOff, int PowOff, class C, class V, class Lds, class Tw,
+          class Sink, int R, int... Rest>
+__device__ __forceinline__ void stockham_from(V (&v)[E], int t, const Tw& tw, const Lds& lds, Sink& sink) {
     constexpr int T = N / E;
     constexpr int NB = E / R;
     static_assert(E % R == 0, "radix must divide elements per thread");
@@ -439,16 +479,13 @@ __device__ __forceinline__ void stockham_pass(C (&v)[E], int t, const Tw& tw, co
         C u[R];
         static_for<R>([&](auto rc) {
             constexpr int r = decltype(rc)::value;
-            u[r] = v[k + r * NB];
+            u[r] = cv<C>(v[k + r * NB]);
         });
         if constexpr (Ns > 1) tw.template apply<TwOff, RegOff, PowOff, R, Ns, INV>(u, k, j);
         Dft<R, INV, C>::run(u);
         if constexpr (sizeof...(Rest) == 0) {
-            // last pass: Ns * R == N, so b < Ns and output r lands in slot k + r NB
-            static_for<R>([&](auto rc) {
-                constexpr int r = decltype(rc)::value;
-                v[k + r * NB] = u[r];
-            });
+            // last pass: Ns * R == N, so b < Ns and output r belongs in slot k + r NB
+            sink(kc, u);
         } else {
             const int o = (b / Ns) * Ns * R + j;
             static_for<R>([&](auto rc) {
@@ -456,32 +493,144 @@ __device__ __forceinline__ void stockham_pass(C (&v)[E], int t, const Tw& tw, co
                 lds.store(o + r * Ns, u[r]);
             });
         }
+#if SLM_GROUP_FENCE
+        // keep butterfly groups apart in the schedule: bounds the live registers
+        // to about one group's worth in the compute type
+        __builtin_amdgcn_sched_barrier(0);
+#endif
     });
     if constexpr (sizeof...(Rest) > 0) {
         exchange_barrier();
         static_for<E>([&](auto mc) {
             constexpr int m = decltype(mc)::value;
-            v[m] = lds.template load<C>(t + m * T);
+            v[m] = lds.template load<V>(t + m * T);
         });
         exchange_barrier();
         constexpr int kNextReg = RegOff + (Ns > 1 ? NB * (R - 1) : 0);
         constexpr int kNextOff = TwOff + (Ns > 1 ? (R - 1) * Ns : 0);
         constexpr int kNextPow = PowOff + (Ns > 1 ? NB : 0);
-        stockham_pass<N, E, INV, Ns * R, kNextOff, kNextReg, kNextPow, C, Lds, Tw, Rest...>(v, t, tw, lds);
+        stockham_from<N, E, INV, Ns * R, kNextOff, kNextReg, kNextPow, C, V, Lds, Tw, Sink, Rest...>(v, t, tw, lds,
+                                                                                                   sink);
     }
 }
 
-template <int K, bool INV, class C, class Lds, class Tw, int... Rs>
-__device__ __forceinline__ void fft_line_impl(C (&v)[PlanOf<K>::E], int t, const Tw& tw, const Lds& lds,
-                                              IntList<Rs...>) {
-    stockham_pass<PlanOf<K>::N, PlanOf<K>::E, INV, 1, 0, 0, 0, C, Lds, Tw, Rs...>(v, t, tw, lds);
+template <int... Rs>
+struct FirstOf;
+template <int R0, int... Rs>
+struct FirstOf<R0, Rs...> {
+    static constexpr int value = R0;
+};
+template <int... Rs>
+struct LastOf {
+    static constexpr int vals[] = {Rs...};
+    static constexpr int value = vals[sizeof...(Rs) - 1];
+};
+
+// Re-load twiddles per transform (no reuse across the pair) where a thread
+// holds 16+ elements: there the reuse costs more registers than the loads.
+template <int K>
+constexpr bool kLaunder = PlanOf<K>::E >= 16;
+
+// whole transform, starting at pass 0
+template <int K, bool INV, class C, class V, class Lds, class Tw, class Sink, int... Rs>
+__device__ __forceinline__ void stockham_all(V (&v)[PlanOf<K>::E], int t, const Tw& tw0, const Lds& lds, Sink& sink,
+                                             IntList<Rs...>) {
+    Tw tw = tw0;
+    if constexpr (kLaunder<K>) tw.launder();
+    stockham_from<PlanOf<K>::N, PlanOf<K>::E, INV, 1, 0, 0, 0, C, V, Lds, Tw, Sink, Rs...>(v, t, tw, lds, sink);
+}
+// passes 1.. of a transform whose first pass already wrote the LDS line
+// (pass 0 has no twiddles, so every twiddle offset is still 0 here)
+template <int K, bool INV, class C, class V, class Lds, class Tw, class Sink, int R0, int... Rs>
+__device__ __forceinline__ void stockham_after_first(V (&v)[PlanOf<K>::E], int t, const Tw& tw0, const Lds& lds,
+                                                     Sink& sink, IntList<R0, Rs...>) {
+    static_assert(sizeof...(Rs) > 0, "fused transforms need at least two passes");
+    Tw tw = tw0;
+    if constexpr (kLaunder<K>) tw.launder();
+    stockham_from<PlanOf<K>::N, PlanOf<K>::E, INV, R0, 0, 0, 0, C, V, Lds, Tw, Sink, Rs...>(v, t, tw, lds, sink);
 }
 
+template <int... Rs>
+constexpr int first_radix(IntList<Rs...>) { return FirstOf<Rs...>::value; }
+template <int... Rs>
+constexpr int last_radix(IntList<Rs...>) { return LastOf<Rs...>::value; }
+
+// Writes the last pass back to the slots.
+template <int E, class V>
+struct WriteBack {
+    V (&v)[E];
+    template <class KC, class C, int R>
+    __device__ __forceinline__ void operator()(KC, C (&u)[R]) const {
+        constexpr int k = KC::value, NB = E / R;
+        static_for<R>([&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            v[k + r * NB] = cv<V>(u[r]);
+        });
+    }
+};
+
 // Transform one line held in the slot layout. Every thread of the workgroup
-// must call this (it contains workgroup barriers).
-template <int K, bool INV, class C, class Lds, class Tw>
-__device__ __forceinline__ void fft_line(C (&v)[PlanOf<K>::E], int t, const Tw& tw, const Lds& lds) {
-    fft_line_impl<K, INV, C>(v, t, tw, lds, RadicesOf<K>{});
+// must call these (they contain workgroup barriers).
+template <int K, bool INV, class C, class V, class Lds, class Tw>
+__device__ __forceinline__ void fft_line(V (&v)[PlanOf<K>::E], int t, const Tw& tw, const Lds& lds) {
+    WriteBack<PlanOf<K>::E, V> wb{v};
+    stockham_all<K, INV, C>(v, t, tw, lds, wb, RadicesOf<K>{});
+}
+
+// Transform, then epi(slot m, C& z) on every output in the compute type, then
+// write back.
+template <int K, bool INV, class C, class V, class Lds, class Tw, class Epi>
+__device__ __forceinline__ void fft_line_epi(V (&v)[PlanOf<K>::E], int t, const Tw& tw, const Lds& lds, Epi&& epi) {
+    constexpr int E = PlanOf<K>::E;
+    auto sink = [&](auto kc, auto& u) {
+        constexpr int k = decltype(kc)::value;
+        constexpr int R = sizeof(u) / sizeof(u[0]);
+        constexpr int NB = E / R;
+        static_for<R>([&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            epi(k + r * NB, u[r]);
+            v[k + r * NB] = cv<V>(u[r]);
+        });
+    };
+    stockham_all<K, INV, C>(v, t, tw, lds, sink, RadicesOf<K>{});
+}
+
+// Transform (INV1), epi(slot m, C& z) on every output, transform (INV2).
+template <int K, bool INV1, bool INV2, class C, class V, class Lds, class Tw, class Epi>
+__device__ __forceinline__ void fft_pair(V (&v)[PlanOf<K>::E], int t, const Tw& tw, const Lds& lds, Epi&& epi) {
+    constexpr int E = PlanOf<K>::E;
+    constexpr int T = PlanOf<K>::T;
+    constexpr int R0 = first_radix(RadicesOf<K>{});
+    constexpr int RL = last_radix(RadicesOf<K>{});
+    if constexpr (SLM_FUSE_PAIR && R0 == RL && kPlans[K].npass > 1) {
+        // group k of the last pass is group k of the next transform's first pass
+        auto sink = [&](auto kc, auto& u) {
+            constexpr int k = decltype(kc)::value;
+            constexpr int NB = E / RL;
+            static_for<RL>([&](auto rc) {
+                constexpr int r = decltype(rc)::value;
+                epi(k + r * NB, u[r]);
+            });
+            Dft<RL, INV2, C>::run(u);  // first pass: Ns = 1, no twiddles
+            const int o = (t + k * T) * RL;
+            static_for<RL>([&](auto rc) {
+                constexpr int r = decltype(rc)::value;
+                lds.store(o + r, u[r]);
+            });
+        };
+        stockham_all<K, INV1, C>(v, t, tw, lds, sink, RadicesOf<K>{});
+        exchange_barrier();
+        static_for<E>([&](auto mc) {
+            constexpr int m = decltype(mc)::value;
+            v[m] = lds.template load<V>(t + m * T);
+        });
+        exchange_barrier();
+        WriteBack<E, V> wb{v};
+        stockham_after_first<K, INV2, C>(v, t, tw, lds, wb, RadicesOf<K>{});
+    } else {
+        fft_line_epi<K, INV1, C>(v, t, tw, lds, epi);
+        fft_line<K, INV2, C>(v, t, tw, lds);
+    }
 }
 
 }  // namespace slm

@@ -21,6 +21,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "fft_core.hpp"
 
 namespace slm {
@@ -100,10 +102,20 @@ enum Precision : int { PREC_F32 = 0, PREC_F64 = 1, PREC_NUM = 2 };
 // ------------------------------------------------------------------------
 // geometry
 // ------------------------------------------------------------------------
+// Workgroups of both passes keep their LDS at <= 80 KiB where the line allows,
+// so two of them share a CU and one's loads overlap the other's transforms.
+constexpr int kLdsPair = 80 * 1024;
+#ifndef SLM_ROW_PAIRS
+#define SLM_ROW_PAIRS 0  // measured equal at 4096 (row quads kept: whole 128-B lines)
+#endif
+
 template <int K>  // plan key of the row length
 struct RowCfg {
     static constexpr int T = PlanOf<K>::T;
-    static constexpr int RPW = (T >= 64) ? 4 : 256 / T;  // rows per workgroup, a multiple of 4
+    // rows per workgroup: a row quad (whole 128-B lines of the blocked layout),
+    // or a row pair for lines too long for two quads per CU
+    static constexpr int RPW = (T >= 64) ? (SLM_ROW_PAIRS && 4 * PlanOf<K>::ROWSTRIDE * 8 > kLdsPair ? 2 : 4) : 256 / T;
+    static constexpr int QR = RPW < 4 ? RPW : 4;  // rows interleaved across a wave
     static constexpr int THREADS = RPW * T;
 };
 
@@ -232,6 +244,11 @@ __device__ __forceinline__ void block_reduce_stats(double& mx, double& s2, doubl
     }
 }
 
+// state type between passes: complex64 when the exchange is complex64 (see
+// fft_core.hpp, Stockham driver), else the compute type
+template <int P, class X>
+using StateOf = std::conditional_t<std::is_same_v<X, float2>, float2, CplxOf<P>>;
+
 // ------------------------------------------------------------------------
 // row pass
 // ------------------------------------------------------------------------
@@ -246,6 +263,7 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS) row_kernel(RowParams p) {
     constexpr int LINE = PlanOf<K>::ROWSTRIDE;
     constexpr int TL = T < 16 ? T : 16;
     using X = XchgOf<P, (long long)RPW * LINE, K>;
+    using V = StateOf<P, X>;
     __shared__ X smem[RPW * LINE];
 
     const int b = blockIdx.y;
@@ -253,12 +271,13 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS) row_kernel(RowParams p) {
     // one row, then the next row of the quad. One wave instruction touches
     // 16 consecutive x of 4 rows = four whole 128-B lines of the blocked layout,
     // and a 16-lane LDS write group stays inside one row.
+    constexpr int QR = RowCfg<K>::QR;
     const int tlo = threadIdx.x % TL;
-    const int q4 = (threadIdx.x / TL) & 3;
-    const int rest = threadIdx.x / (4 * TL);
+    const int q4 = (threadIdx.x / TL) % QR;
+    const int rest = threadIdx.x / (QR * TL);
     const int qq = rest / (T / TL);
     const int t = tlo + TL * (rest - qq * (T / TL));
-    const int lrow = qq * 4 + q4;
+    const int lrow = qq * QR + q4;
     const int row = blockIdx.x * RPW + lrow;
     const long long hoff = (long long)b * p.holo;
     const long long roff = (long long)row * W;                  // row-major (user arrays)
@@ -267,7 +286,7 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS) row_kernel(RowParams p) {
     const LdsLine<X> lds{smem + lrow * LINE};
     Twiddles<K, C, tw_mode<P, RowCfg<K>::THREADS>()> tw;
     load_twiddles<K, C>(tw, t, p.tw);
-    C v[E];
+    V v[E];
 
     auto ain_at = [&](int m) -> S { return p.ain ? (S)p.ain[roff + t + T * m] : (S)1; };
 
@@ -280,14 +299,14 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS) row_kernel(RowParams p) {
             else
                 sincos((double)p.phase_in[hoff + roff + t + T * m], &sn, &cs);
             const S a = ain_at(m);
-            v[m] = mk<C>(a * cs, a * sn);
+            v[m] = cv<V>(mk<C>(a * cs, a * sn));
         }
     } else if constexpr (MODE == ROW_GD_INIT_FIELD) {
 #pragma unroll
-        for (int m = 0; m < E; ++m) v[m] = normalize(from_c64<C>(p.field[boff + m * bstep]), ain_at(m));
+        for (int m = 0; m < E; ++m) v[m] = cv<V>(normalize(from_c64<C>(p.field[boff + m * bstep]), ain_at(m)));
     } else {
 #pragma unroll
-        for (int m = 0; m < E; ++m) v[m] = from_c64<C>(p.in[boff + m * bstep]);
+        for (int m = 0; m < E; ++m) v[m] = cv<V>(p.in[boff + m * bstep]);
     }
     // the stop test is issued behind the loads so its latency overlaps them
     if constexpr (MODE == ROW_GS_MAIN) {
@@ -296,59 +315,50 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS) row_kernel(RowParams p) {
         if (p.iter > p.stop_iter[b]) return;
     }
 
-    if constexpr (MODE == ROW_GS_MAIN || MODE == ROW_GS_PHASE || MODE == ROW_GD_INIT_Y || MODE == ROW_GD_MAIN ||
-                  MODE == ROW_FFT_INV) {
-        fft_line<K, true>(v, t, tw, lds);
-    }
-
     if constexpr (MODE == ROW_GS_PHASE) {
-#pragma unroll
-        for (int m = 0; m < E; ++m) p.phase_out[hoff + roff + t + T * m] = (float)atan2(v[m].y, v[m].x);
+        fft_line_epi<K, true, C>(v, t, tw, lds, [&](int m, C& z) {
+            p.phase_out[hoff + roff + t + T * m] = (float)atan2(z.y, z.x);
+        });
         return;
-    } else if constexpr (MODE == ROW_FFT_INV) {
-#pragma unroll
-        for (int m = 0; m < E; ++m) p.out[boff + m * bstep] = to_c64(v[m]);
-        return;
-    } else {
-        if constexpr (MODE == ROW_GS_MAIN) {
-#pragma unroll
-            for (int m = 0; m < E; ++m) v[m] = unit_scale(v[m], ain_at(m));
-        } else if constexpr (MODE == ROW_GD_INIT_Y) {
-#pragma unroll
-            for (int m = 0; m < E; ++m) {
-                const S a = ain_at(m);
-                const C x = unit_scale(v[m], a);  // a_in exp(i angle(ifft2(sqrt T)))
-                p.field[boff + m * bstep] = to_c64(x);
-                v[m] = normalize(x, a);
-            }
-        } else if constexpr (MODE == ROW_GD_MAIN) {
-            // dEdF = ifft2(...) * a_in (src/algorithms.py:87-89); dEdX_complex (:179-185);
-            // input -= lr * dEdX (:91); next forward input x/|x| a_in (:84).
-            const S lr = (S)p.lr[p.iter];
-            const S inv_s = (S)1 / (S)p.holo;
-#pragma unroll
-            for (int m = 0; m < E; ++m) {
-                const S a = ain_at(m);
-                const C g = mk<C>(v[m].x * inv_s * a, v[m].y * inv_s * a);
-                const long long idx = boff + m * bstep;
-                C x = from_c64<C>(p.field[idx]);
-                const S ax2 = x.x * x.x + x.y * x.y;
-                const S inv = rsqrt_nr(ax2);
-                const S inv3 = inv * inv * inv;
-                const S re = x.x * g.x + x.y * g.y;
-                const S dx = g.x * inv - x.x * re * inv3;
-                const S dy = g.y * inv - x.y * re * inv3;
-                x.x -= lr * dx;
-                x.y -= lr * dy;
-                const float2 xs = to_c64(x);  // the field is stored in complex64
-                p.field[idx] = xs;
-                v[m] = normalize(from_c64<C>(xs), a);
-            }
-        }
-        fft_line<K, false>(v, t, tw, lds);
-#pragma unroll
-        for (int m = 0; m < E; ++m) p.out[boff + m * bstep] = to_c64(v[m]);
+    } else if constexpr (MODE == ROW_FFT_INV || MODE == ROW_FFT_FWD) {
+        fft_line<K, MODE == ROW_FFT_INV, C>(v, t, tw, lds);
+    } else if constexpr (MODE == ROW_PHASE_FWD || MODE == ROW_GD_INIT_FIELD) {
+        fft_line<K, false, C>(v, t, tw, lds);
+    } else if constexpr (MODE == ROW_GS_MAIN) {
+        // A -> B = a_in A/|A| (src/algorithms.py:30)
+        fft_pair<K, true, false, C>(v, t, tw, lds, [&](int m, C& z) { z = unit_scale(z, ain_at(m)); });
+    } else if constexpr (MODE == ROW_GD_INIT_Y) {
+        fft_pair<K, true, false, C>(v, t, tw, lds, [&](int m, C& z) {
+            const S a = ain_at(m);
+            const C x = unit_scale(z, a);  // a_in exp(i angle(ifft2(sqrt T)))
+            p.field[boff + m * bstep] = to_c64(x);
+            z = normalize(x, a);
+        });
+    } else if constexpr (MODE == ROW_GD_MAIN) {
+        // dEdF = ifft2(...) * a_in (src/algorithms.py:87-89); dEdX_complex (:179-185);
+        // input -= lr * dEdX (:91); next forward input x/|x| a_in (:84).
+        const S lr = (S)p.lr[p.iter];
+        const S inv_s = (S)1 / (S)p.holo;
+        fft_pair<K, true, false, C>(v, t, tw, lds, [&](int m, C& z) {
+            const S a = ain_at(m);
+            const C g = mk<C>(z.x * inv_s * a, z.y * inv_s * a);
+            const long long idx = boff + m * bstep;
+            C x = from_c64<C>(p.field[idx]);
+            const S ax2 = x.x * x.x + x.y * x.y;
+            const S inv = rsqrt_nr(ax2);
+            const S inv3 = inv * inv * inv;
+            const S re = x.x * g.x + x.y * g.y;
+            const S dx = g.x * inv - x.x * re * inv3;
+            const S dy = g.y * inv - x.y * re * inv3;
+            x.x -= lr * dx;
+            x.y -= lr * dy;
+            const float2 xs = to_c64(x);  // the field is stored in complex64
+            p.field[idx] = xs;
+            z = normalize(from_c64<C>(xs), a);
+        });
     }
+#pragma unroll
+    for (int m = 0; m < E; ++m) p.out[boff + m * bstep] = cv<float2>(v[m]);
 }
 
 // ------------------------------------------------------------------------
@@ -364,6 +374,7 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS)) col_kernel(ColParams
     constexpr int LINE = PlanOf<K>::LINE;
     constexpr int THREADS = ColCfg<K, CW>::THREADS;
     using X = XchgOf<P, (long long)LINE * CW, K>;
+    using V = StateOf<P, X>;
     __shared__ X smem[LINE * CW];
 
     const int b = blockIdx.y;
@@ -377,7 +388,9 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS)) col_kernel(ColParams
     const LdsTile<CW, X> lds{smem, c};
     Twiddles<K, C, tw_mode<P, THREADS>()> tw;
     load_twiddles<K, C>(tw, t, p.tw);
-    C v[E];
+    V v[E];
+    constexpr bool kTarget = (MODE == COL_GS_MAIN || MODE == COL_GD_STATS || MODE == COL_GD_GRAD);
+    float tv[kTarget ? E : 1];
 
     // GD gradient needs this iteration's global max of |F|^2 (src/algorithms.py:86).
     S maxp = 0;
@@ -396,66 +409,65 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS)) col_kernel(ColParams
     if constexpr (MODE == COL_REAL_INV) {
 #pragma unroll
         for (int m = 0; m < E; ++m) {
-            const float tv = TgtLoad<TT>::load(p.tgt, base + m * kStep);
-            v[m] = mk<C>((S)TgtLoad<TT>::amp(tv), (S)0);
+            const float a = TgtLoad<TT>::amp(TgtLoad<TT>::load(p.tgt, base + m * kStep));
+            v[m] = cv<V>(mk<C>((S)a, (S)0));
         }
     } else if constexpr (MODE == COL_EXPECTED) {
         // GD keeps X of iteration i in buffer i % 2; GS passes the same buffer twice.
         const int s = min(p.stop_iter[b], p.loops - 1);
         const float2* src = (s & 1) ? p.in_alt : p.in;
 #pragma unroll
-        for (int m = 0; m < E; ++m) v[m] = from_c64<C>(src[base + m * kStep]);
+        for (int m = 0; m < E; ++m) v[m] = cv<V>(src[base + m * kStep]);
     } else {
 #pragma unroll
-        for (int m = 0; m < E; ++m) v[m] = from_c64<C>(p.in[base + m * kStep]);
+        for (int m = 0; m < E; ++m) v[m] = cv<V>(p.in[base + m * kStep]);
+    }
+    if constexpr (kTarget) {
+        // the target is consumed in the middle of the kernel: fetch it up front
+#pragma unroll
+        for (int m = 0; m < E; ++m) tv[m] = TgtLoad<TT>::load(p.tgt, base + m * kStep);
     }
     // the stop test is issued behind the loads so its latency overlaps them
-    if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_STATS || MODE == COL_GD_GRAD) {
+    if constexpr (kTarget) {
         if (p.iter > p.stop_iter[b]) return;
     }
 
-    if constexpr (MODE == COL_REAL_INV || MODE == COL_FFT_INV) {
-        fft_line<K, true>(v, t, tw, lds);
+    if constexpr (MODE == COL_REAL_INV || MODE == COL_FFT_INV || MODE == COL_FFT_FWD) {
+        fft_line<K, MODE != COL_FFT_FWD, C>(v, t, tw, lds);
 #pragma unroll
-        for (int m = 0; m < E; ++m) p.out[base + m * kStep] = to_c64(v[m]);
-        return;
-    } else {
-        fft_line<K, false>(v, t, tw, lds);
-    }
-
-    if constexpr (MODE == COL_FFT_FWD) {
-#pragma unroll
-        for (int m = 0; m < E; ++m) p.out[base + m * kStep] = to_c64(v[m]);
+        for (int m = 0; m < E; ++m) p.out[base + m * kStep] = cv<float2>(v[m]);
         return;
     } else if constexpr (MODE == COL_EXPECTED) {
         const long long nat = (long long)b * p.holo + (long long)t * p.W + x;  // row-major output
-#pragma unroll
-        for (int m = 0; m < E; ++m)
-            p.e_out[nat + (long long)m * T * p.W] = (float)(v[m].x * v[m].x + v[m].y * v[m].y);
+        fft_line_epi<K, false, C>(v, t, tw, lds, [&](int m, C& z) {
+            p.e_out[nat + (long long)m * T * p.W] = (float)(z.x * z.x + z.y * z.y);
+        });
         return;
     } else {
         double mx = 0.0, s2 = 0.0, st = 0.0;
         const S norm = (MODE == COL_GD_GRAD) ? (S)p.norm[b] : (S)0;
-#pragma unroll
-        for (int m = 0; m < E; ++m) {
-            const float tv = TgtLoad<TT>::load(p.tgt, base + m * kStep);
-            const S e = v[m].x * v[m].x + v[m].y * v[m].y;
+        auto epi = [&](int m, C& z) {
+            const S e = z.x * z.x + z.y * z.y;
             if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_STATS) {
                 // |C|^2 as the reference's float64 expected_outcome sees it
                 const double ed = (double)(float)e;
                 mx = fmax(mx, ed);
                 s2 += ed * ed;
-                st += ed * (double)tv;
+                st += ed * (double)tv[m];
             }
             if constexpr (MODE == COL_GS_MAIN) {
-                v[m] = unit_scale(v[m], (S)TgtLoad<TT>::amp(tv));
+                z = unit_scale(z, (S)TgtLoad<TT>::amp(tv[m]));  // D = a_T C/|C| (src/algorithms.py:33)
             } else if constexpr (MODE == COL_GD_GRAD) {
                 // mask * F * (output - T), output = |F|^2 norm / max (src/algorithms.py:80,85-88)
                 const S o = e * norm / maxp;
-                const S w = ((S)1 + (S)p.wa * (S)tv / (S)255) * (o - (S)tv);
-                v[m] = mk<C>(v[m].x * w, v[m].y * w);
+                const S w = ((S)1 + (S)p.wa * (S)tv[m] / (S)255) * (o - (S)tv[m]);
+                z = mk<C>(z.x * w, z.y * w);
             }
-        }
+        };
+        if constexpr (MODE == COL_GD_STATS)
+            fft_line_epi<K, false, C>(v, t, tw, lds, epi);
+        else
+            fft_pair<K, false, true, C>(v, t, tw, lds, epi);
         if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_STATS) {
             block_reduce_stats<THREADS>(mx, s2, st);
             if (threadIdx.x == 0) {
@@ -467,9 +479,8 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS)) col_kernel(ColParams
             }
         }
         if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD) {
-            fft_line<K, true>(v, t, tw, lds);
 #pragma unroll
-            for (int m = 0; m < E; ++m) p.out[base + m * kStep] = to_c64(v[m]);
+            for (int m = 0; m < E; ++m) p.out[base + m * kStep] = cv<float2>(v[m]);
         }
     }
 }

@@ -23,21 +23,29 @@ struct RadixPlan {
 // SLM height of the reference CLI (src/constants.py:5-6).
 // Kernel templates are keyed by the index into this table (the "plan key").
 // Wide plans minimise passes; narrow plans halve the work per thread so a
-// single small image still puts several waves on every SIMD.
+// single small image still puts several waves on every SIMD. First and last
+// radix are equal wherever the length allows, so the projection between an
+// inverse and a forward transform runs inside one butterfly group
+// (fft_core.hpp, fft_pair).
+// 4096: 32 elements per thread in radix-8 passes (512-thread column tiles,
+// no float64 spills); -DSLM_PLAN4096 selects experimental variants
+#ifndef SLM_PLAN4096
+#define SLM_PLAN4096 {4096, 32, 0, 4, {8, 8, 8, 8}}
+#endif
 constexpr RadixPlan kPlans[] = {
     {64, 8, 0, 2, {8, 8, 0, 0}},
-    {128, 16, 0, 2, {16, 8, 0, 0}},
+    {128, 16, 0, 3, {4, 8, 4, 0}},
     {256, 16, 0, 2, {16, 16, 0, 0}},
-    {512, 16, 0, 3, {16, 16, 2, 0}},
-    {768, 24, 0, 3, {12, 8, 8, 0}},
-    {1024, 16, 0, 3, {16, 16, 4, 0}},
-    {2048, 16, 0, 3, {16, 16, 8, 0}},
-    {4096, 16, 0, 3, {16, 16, 16, 0}},
-    {256, 8, 1, 3, {8, 8, 4, 0}},
+    {512, 16, 0, 3, {16, 2, 16, 0}},
+    {768, 24, 0, 3, {8, 12, 8, 0}},
+    {1024, 16, 0, 3, {16, 4, 16, 0}},
+    {2048, 16, 0, 3, {16, 8, 16, 0}},
+    SLM_PLAN4096,
+    {256, 8, 1, 3, {8, 4, 8, 0}},
     {512, 8, 1, 3, {8, 8, 8, 0}},
-    {768, 12, 1, 4, {12, 4, 4, 4}},
-    {1024, 8, 1, 4, {8, 8, 4, 4}},
-    {2048, 8, 1, 4, {8, 8, 8, 4}},
+    {768, 12, 1, 4, {4, 12, 4, 4}},
+    {1024, 8, 1, 4, {8, 4, 4, 8}},
+    {2048, 8, 1, 4, {8, 4, 8, 8}},
 };
 constexpr int kNumPlans = sizeof(kPlans) / sizeof(kPlans[0]);
 

@@ -213,14 +213,15 @@ struct slm_plan {
 namespace {
 
 // Column tile width. With the blocked state layout a 4-column panel is one
-// contiguous run, so the narrowest tile already moves whole lines and keeps
-// the most workgroups (and LDS headroom) per CU; SLM_COL_CW overrides.
+// contiguous run, so a 4-column tile moves whole lines (2-column tiles, which
+// rely on the partner tile fetching the other half of each line through the
+// same XCD's L2, measured slower at 4096). SLM_COL_CW overrides.
 int pick_cw(int ck, int W) {
     if (const char* s = std::getenv("SLM_COL_CW")) {
         const int cw = std::atoi(s);
         if (col_fn(ck, cw, COL_GS_MAIN, TGT_F32, PREC_F32) && W % cw == 0) return cw;
     }
-    for (int cw : {4, 8, 16})
+    for (int cw : {4, 8, 16, 2})
         if (W % cw == 0 && col_fn(ck, cw, COL_GS_MAIN, TGT_F32, PREC_F32)) return cw;
     return 0;
 }
