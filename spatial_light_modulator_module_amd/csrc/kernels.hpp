@@ -40,6 +40,7 @@ struct RowParams {
     const float* lr;         // GD learning rate per iteration
     const int* stop_iter;    // [B], INT_MAX while running
     int iter;                // iteration index of this launch
+    int wt;                  // write-through field stores (store_field)
     int W;                   // row length (== template W; kept for checks)
     int H;                   // rows per hologram (column stride of the blocked layout)
     long long holo;          // elements per hologram (H * W)
@@ -59,6 +60,7 @@ struct ColParams {
     int iter;                // iteration index of this launch
     int max_loops;           // partial-slab stride
     int loops;               // iterations of this run
+    int wt;                  // write-through field stores (store_field)
     int W;                   // image width (row stride)
     int nwg;                 // column workgroups per hologram (W / CW)
     long long holo;          // elements per hologram
@@ -113,8 +115,11 @@ template <int K>  // plan key of the row length
 struct RowCfg {
     static constexpr int T = PlanOf<K>::T;
     // rows per workgroup: a row quad (whole 128-B lines of the blocked layout),
-    // or a row pair for lines too long for two quads per CU
-    static constexpr int RPW = (T >= 64) ? (SLM_ROW_PAIRS && 4 * PlanOf<K>::ROWSTRIDE * 8 > kLdsPair ? 2 : 4) : 256 / T;
+    // or a row pair when a quad would not leave room for two workgroups per CU
+    // and a pair still fills 8 waves (the partner pair, which reads the other
+    // half of each 128-B line, is placed on the same XCD: row_kernel remap)
+    static constexpr bool kPairs = 4 * PlanOf<K>::ROWSTRIDE * 8 > kLdsPair && (SLM_ROW_PAIRS || T >= 256);
+    static constexpr int RPW = (T >= 64) ? (kPairs ? 2 : 4) : 256 / T;
     static constexpr int QR = RPW < 4 ? RPW : 4;  // rows interleaved across a wave
     static constexpr int THREADS = RPW * T;
 };
@@ -126,6 +131,27 @@ struct ColCfg {
     static constexpr bool kValid =
         THREADS >= 64 && THREADS <= 1024 && lds_line(PlanOf<K>::N) * CW * 8 <= 160 * 1024;
 };
+
+// Waves per SIMD that the LDS footprint of a workgroup allows, handed to the
+// compiler as amdgpu_waves_per_eu (second __launch_bounds__ argument) so that
+// register allocation does not cap occupancy below what LDS permits (e.g. the
+// batched 1024 tiles: 35 KB of LDS would allow four workgroups per CU, but 150-200
+// VGPRs held them to two). Capped at SLM_MAX_WPE (4 => <= 128 VGPRs).
+#ifndef SLM_OCC
+#define SLM_OCC 0  // measured: the forced 128-VGPR cap spills the float64 transforms (slower everywhere)
+#endif
+#ifndef SLM_MAX_WPE
+#define SLM_MAX_WPE 4
+#endif
+constexpr int occupancy_wpe(int threads, long long lds_bytes) {
+    const int waves = (threads + 63) / 64;
+    long long wgs = lds_bytes > 0 ? (160LL * 1024) / lds_bytes : 64;
+    if (wgs < 1) wgs = 1;
+    long long wpe = wgs * waves / 4;
+    if (wpe < 1) wpe = 1;
+    if (wpe > SLM_MAX_WPE) wpe = SLM_MAX_WPE;
+    return SLM_OCC ? (int)wpe : 1;
+}
 
 // XCD-aware bijective remap: blocks that share (id % 8) — one XCD under the
 // observed round-robin dispatch — get consecutive logical column groups, so
@@ -177,6 +203,18 @@ __device__ __forceinline__ C normalize(C x, Scalar<C> a) {
     return mk<C>(x.x * r * a, x.y * r * a);
 }
 
+// Field stores of the iteration passes. wt = write-through (agent-scope
+// relaxed atomic store = global_store sc1): the bytes go to memory as they are
+// stored, so the kernel ends with no dirty L2 lines to write back before the
+// dependent launch (MI355X_MICROARCH.md: a boundary costs + dirty bytes / 6 TB/s).
+__device__ __forceinline__ void store_field(float2* dst, float2 v, int wt) {
+    if (wt)
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(dst), __builtin_bit_cast(unsigned long long, v),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+        *dst = v;
+}
+
 template <int P>
 using CplxOf = std::conditional_t<P == 0, float2, double2>;
 
@@ -194,9 +232,9 @@ template <int P, long long SLOTS, int K>
 using XchgOf = std::conditional_t<((SLM_F64_XCHG || kPlans[K].variant == 1) && P == 1 && SLOTS * 16 <= 80 * 1024),
                                   double2, float2>;
 
-template <int P, int THREADS>
+template <int P, int THREADS, int K>
 constexpr int tw_mode() {
-    return P == 1 ? SLM_F64_TW : (THREADS <= 512 ? TW_CACHED : TW_DIRECT);
+    return P == 1 ? SLM_F64_TW : (THREADS <= 512 && PlanOf<K>::E <= 16 ? TW_CACHED : TW_DIRECT);
 }
 
 template <int TT>
@@ -252,8 +290,14 @@ using StateOf = std::conditional_t<std::is_same_v<X, float2>, float2, CplxOf<P>>
 // ------------------------------------------------------------------------
 // row pass
 // ------------------------------------------------------------------------
+template <int K, int P>
+constexpr int row_wpe() {
+    using X = XchgOf<P, (long long)RowCfg<K>::RPW * PlanOf<K>::ROWSTRIDE, K>;
+    return occupancy_wpe(RowCfg<K>::THREADS, (long long)RowCfg<K>::RPW * PlanOf<K>::ROWSTRIDE * sizeof(X));
+}
+
 template <int K, int MODE, int P>
-__global__ void __launch_bounds__(RowCfg<K>::THREADS) row_kernel(RowParams p) {
+__global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_kernel(RowParams p) {
     using C = CplxOf<P>;
     using S = Scalar<C>;
     constexpr int W = PlanOf<K>::N;
@@ -278,13 +322,14 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS) row_kernel(RowParams p) {
     const int qq = rest / (T / TL);
     const int t = tlo + TL * (rest - qq * (T / TL));
     const int lrow = qq * QR + q4;
-    const int row = blockIdx.x * RPW + lrow;
+    // consecutive row groups on one XCD (row pairs share 128-B lines through its L2)
+    const int row = xcd_remap(blockIdx.x, gridDim.x) * RPW + lrow;
     const long long hoff = (long long)b * p.holo;
     const long long roff = (long long)row * W;                  // row-major (user arrays)
     const long long boff = hoff + blk_index(row, t, p.H);        // blocked (state), slot m adds m*T*H
     const long long bstep = (long long)T * p.H;
     const LdsLine<X> lds{smem + lrow * LINE};
-    Twiddles<K, C, tw_mode<P, RowCfg<K>::THREADS>()> tw;
+    Twiddles<K, C, tw_mode<P, RowCfg<K>::THREADS, K>()> tw;
     load_twiddles<K, C>(tw, t, p.tw);
     V v[E];
 
@@ -358,14 +403,20 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS) row_kernel(RowParams p) {
         });
     }
 #pragma unroll
-    for (int m = 0; m < E; ++m) p.out[boff + m * bstep] = cv<float2>(v[m]);
+    for (int m = 0; m < E; ++m) store_field(p.out + boff + m * bstep, cv<float2>(v[m]), p.wt);
 }
 
 // ------------------------------------------------------------------------
 // column pass
 // ------------------------------------------------------------------------
+template <int K, int CW, int P>
+constexpr int col_wpe() {
+    using X = XchgOf<P, (long long)PlanOf<K>::LINE * CW, K>;
+    return occupancy_wpe(ColCfg<K, CW>::THREADS, (long long)PlanOf<K>::LINE * CW * sizeof(X));
+}
+
 template <int K, int CW, int MODE, int TT, int P>
-__global__ void __launch_bounds__((ColCfg<K, CW>::THREADS)) col_kernel(ColParams p) {
+__global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>())) col_kernel(ColParams p) {
     using C = CplxOf<P>;
     using S = Scalar<C>;
     constexpr int H = PlanOf<K>::N;
@@ -386,7 +437,7 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS)) col_kernel(ColParams
     const long long base = (long long)b * p.holo + blk_index(t, x, H);
     constexpr long long kStep = 4LL * T;
     const LdsTile<CW, X> lds{smem, c};
-    Twiddles<K, C, tw_mode<P, THREADS>()> tw;
+    Twiddles<K, C, tw_mode<P, THREADS, K>()> tw;
     load_twiddles<K, C>(tw, t, p.tw);
     V v[E];
     constexpr bool kTarget = (MODE == COL_GS_MAIN || MODE == COL_GD_STATS || MODE == COL_GD_GRAD);
@@ -435,7 +486,7 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS)) col_kernel(ColParams
     if constexpr (MODE == COL_REAL_INV || MODE == COL_FFT_INV || MODE == COL_FFT_FWD) {
         fft_line<K, MODE != COL_FFT_FWD, C>(v, t, tw, lds);
 #pragma unroll
-        for (int m = 0; m < E; ++m) p.out[base + m * kStep] = cv<float2>(v[m]);
+        for (int m = 0; m < E; ++m) store_field(p.out + base + m * kStep, cv<float2>(v[m]), p.wt);
         return;
     } else if constexpr (MODE == COL_EXPECTED) {
         const long long nat = (long long)b * p.holo + (long long)t * p.W + x;  // row-major output
@@ -480,7 +531,7 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS)) col_kernel(ColParams
         }
         if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD) {
 #pragma unroll
-            for (int m = 0; m < E; ++m) p.out[base + m * kStep] = cv<float2>(v[m]);
+            for (int m = 0; m < E; ++m) store_field(p.out + base + m * kStep, cv<float2>(v[m]), p.wt);
         }
     }
 }

@@ -46,6 +46,7 @@ constexpr RadixPlan kPlans[] = {
     {768, 12, 1, 4, {4, 12, 4, 4}},
     {1024, 8, 1, 4, {8, 4, 4, 8}},
     {2048, 8, 1, 4, {8, 4, 8, 8}},
+    {4096, 16, 1, 3, {16, 16, 16, 0}},
 };
 constexpr int kNumPlans = sizeof(kPlans) / sizeof(kPlans[0]);
 

@@ -184,6 +184,7 @@ struct slm_plan {
     long long holo = 0;
     hipStream_t stream = nullptr;
     int prec = PREC_F64;
+    int wt = 1;  // write-through field stores ($SLM_WT=0 disables)
     const void* tw_row = nullptr;
     const void* tw_col = nullptr;
     float2 *xa = nullptr, *xb = nullptr, *y = nullptr, *field = nullptr;
@@ -220,6 +221,14 @@ int pick_cw(int ck, int W) {
     if (const char* s = std::getenv("SLM_COL_CW")) {
         const int cw = std::atoi(s);
         if (col_fn(ck, cw, COL_GS_MAIN, TGT_F32, PREC_F32) && W % cw == 0) return cw;
+    }
+    // first tile (in this order) whose complex64 LDS leaves room for two
+    // workgroups per CU; 2-column tiles only with >= 8 waves (long columns)
+    for (int cw : {4, 8, 16, 2}) {
+        if (W % cw || !col_fn(ck, cw, COL_GS_MAIN, TGT_F32, PREC_F32)) continue;
+        const long long lds = (long long)lds_line(kPlans[ck].n) * cw * 8;
+        const int threads = cw * (kPlans[ck].n / kPlans[ck].e);
+        if (lds <= 80 * 1024 && (cw != 2 || threads >= 512)) return cw;
     }
     for (int cw : {4, 8, 16, 2})
         if (W % cw == 0 && col_fn(ck, cw, COL_GS_MAIN, TGT_F32, PREC_F32)) return cw;
@@ -279,6 +288,7 @@ RowParams row_params(slm_plan* p) {
     r.holo = p->holo;
     r.inv_s = (float)(1.0 / (double)p->holo);
     r.tw = p->tw_row;
+    r.wt = p->wt;
     return r;
 }
 
@@ -294,6 +304,7 @@ ColParams col_params(slm_plan* p) {
     c.nwg = p->nwg;
     c.holo = p->holo;
     c.tw = p->tw_col;
+    c.wt = p->wt;
     return c;
 }
 
@@ -514,6 +525,7 @@ int slm_plan_create(int algo, int batch, int height, int width, int tgt_type, in
     p->col_threads = col_threads(p->col_key, p->cw);
     p->row_threads = row_threads(p->row_key);
     p->rpw = row_rpw(p->row_key);
+    if (const char* e = std::getenv("SLM_WT")) p->wt = std::atoi(e) != 0;
     if (const char* e = std::getenv("SLM_PRECISION")) p->prec = (std::strcmp(e, "f32") == 0) ? PREC_F32 : PREC_F64;
     int rc = get_twiddles(p->row_key, p->prec, &p->tw_row);
     if (!rc) rc = get_twiddles(p->col_key, p->prec, &p->tw_col);
