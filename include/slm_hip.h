@@ -126,6 +126,28 @@ int slm_comm_destroy(void);
  * and synchronised before returning. */
 int slm_plan_gather_phase(slm_plan* plan, const int* counts, int root, float* host_out);
 
+/* ---- SLM frames: trap holograms and 8-bit quantisation ------------------
+ * (element-wise, one launch per call, host buffers in/out)
+ * slm_trap_frames      -> update_hologram(black_image, coords, which)
+ *                         src/move_traps.py:64-68 (phase_out, float64, the
+ *                         angle of ifft2 of a single 255 pixel at (ys[b], xs[b]))
+ *                         fused with display_hologram's quantisation
+ *                         src/move_traps.py:135-139 (frame_out, rule ASTYPE)
+ * slm_quantize         -> mask_hologram(path, mask_arr, ct2pi)
+ *                         src/display_holograms.py:253-266 (.npy branch: SRC_F64 +
+ *                         rule PIL; image branch: SRC_I16) and display_hologram
+ *                         (SRC_F64 + rule ASTYPE)
+ * mask is [height][width] float64 (broadcast over the batch) or NULL; any
+ * output pointer may be NULL.                                              */
+#define SLM_QUANT_ASTYPE 0 /* ((h + mask) % 2pi * ct2pi / 2pi).astype(uint8) */
+#define SLM_QUANT_PIL 1    /* PIL 'F'->'L' (clip, truncate) of ((h + mask) % 2pi) / 2pi * ct2pi */
+#define SLM_SRC_F64 0      /* phase hologram, float64 */
+#define SLM_SRC_I16 1      /* 8-bit hologram image widened to int16 (PIL 'L' -> np.int16) */
+int slm_trap_frames(int batch, int height, int width, const int* ys, const int* xs, const double* mask,
+                    double ct2pi, int rule, double* phase_out, unsigned char* frame_out);
+int slm_quantize(const void* src, int src_type, const double* mask, int batch, int height, int width, double ct2pi,
+                 int rule, unsigned char* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -73,7 +73,15 @@ _SIGNATURES = [
     ("slm_comm_init", _c_int, [_c_int, _c_int, _vp]),
     ("slm_comm_destroy", _c_int, []),
     ("slm_plan_gather_phase", _c_int, [_vp, _vp, _c_int, _vp]),
+    ("slm_trap_frames", _c_int,
+     [_c_int, _c_int, _c_int, _vp, _vp, _vp, _c_double, _c_int, _vp, _vp]),
+    ("slm_quantize", _c_int, [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_double, _c_int, _vp]),
 ]
+
+QUANT_ASTYPE = 0
+QUANT_PIL = 1
+SRC_F64 = 0
+SRC_I16 = 1
 
 _lib = None
 
@@ -292,3 +300,34 @@ def comm_init(nranks: int, rank: int, uid: bytes) -> None:
 
 def comm_destroy() -> None:
     load().slm_comm_destroy()
+
+
+def trap_frames(shape, ys, xs, mask=None, ct2pi=256.0, rule=QUANT_ASTYPE, phase=True, frame=True):
+    """Single-trap holograms (angle of ifft2 of one 255 pixel per trap) and/or
+    their quantised SLM frames, one launch (slm_trap_frames)."""
+    h, w = shape
+    ys = np.ascontiguousarray(ys, dtype=np.int32).reshape(-1)
+    xs = np.ascontiguousarray(xs, dtype=np.int32).reshape(-1)
+    b = ys.size
+    m = None if mask is None else np.ascontiguousarray(mask, dtype=np.float64).reshape(h, w)
+    ph = np.empty((b, h, w), np.float64) if phase else None
+    fr = np.empty((b, h, w), np.uint8) if frame else None
+    init()
+    check(load().slm_trap_frames(b, h, w, ptr(ys), ptr(xs), ptr(m), float(ct2pi), int(rule), ptr(ph), ptr(fr)),
+          "slm_trap_frames")
+    return ph, fr
+
+
+def quantize(src, mask=None, ct2pi=256.0, rule=QUANT_PIL):
+    """8-bit SLM levels of a float64 phase hologram (rule QUANT_ASTYPE / QUANT_PIL)
+    or of an int16 hologram image, plus an optional float64 mask (slm_quantize)."""
+    src = np.asarray(src)
+    src_type = SRC_I16 if src.dtype == np.int16 else SRC_F64
+    a = np.ascontiguousarray(src, dtype=np.int16 if src_type == SRC_I16 else np.float64)
+    h, w = a.shape[-2:]
+    b = int(np.prod(a.shape[:-2])) if a.ndim > 2 else 1
+    m = None if mask is None else np.ascontiguousarray(np.broadcast_to(mask, (h, w)), dtype=np.float64)
+    out = np.empty(a.shape, np.uint8)
+    init()
+    check(load().slm_quantize(ptr(a), src_type, ptr(m), b, h, w, float(ct2pi), int(rule), ptr(out)), "slm_quantize")
+    return out

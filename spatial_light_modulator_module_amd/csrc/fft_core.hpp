@@ -297,7 +297,9 @@ struct TwCountOf<N, IntList<Rs...>> {
 //  TW_POWERS: float64 arithmetic: only w^1 of each butterfly is cached and the
 //             powers w^2..w^(R-1) are formed by multiplication (error ~1e-15,
 //             far below the complex64 storage rounding).
-enum TwMode : int { TW_CACHED = 0, TW_DIRECT = 1, TW_POWERS = 2 };
+//  TW_CHAIN:  as TW_POWERS, but w^r is formed incrementally as it is applied
+//             (w^r = w^(r-1) w), so only two twiddles are ever live.
+enum TwMode : int { TW_CACHED = 0, TW_DIRECT = 1, TW_POWERS = 2, TW_CHAIN = 3 };
 
 template <int N, int Ns, int... Rs>
 struct TwPowCountImpl;
@@ -384,6 +386,23 @@ struct Twiddles<N, C, TW_POWERS> {
         static_for<R - 1>([&](auto rc) {
             constexpr int r = decltype(rc)::value + 1;
             u[r] = INV ? cmulc(u[r], w[r]) : cmul(u[r], w[r]);
+        });
+    }
+};
+
+template <int N, class C>
+struct Twiddles<N, C, TW_CHAIN> {
+    static constexpr int COUNT = TwPowCountOf<N, RadicesOf<N>>::value > 0 ? TwPowCountOf<N, RadicesOf<N>>::value : 1;
+    C w1[COUNT];
+    __device__ __forceinline__ void launder() {}
+    template <int TwOff, int RegOff, int PowOff, int R, int Ns, bool INV>
+    __device__ __forceinline__ void apply(C* u, int k, int) const {
+        const C b = w1[PowOff + k];
+        C w = b;
+        static_for<R - 1>([&](auto rc) {
+            constexpr int r = decltype(rc)::value + 1;
+            u[r] = INV ? cmulc(u[r], w) : cmul(u[r], w);
+            if constexpr (r + 1 < R) w = cmul(w, b);
         });
     }
 };

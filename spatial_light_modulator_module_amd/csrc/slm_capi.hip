@@ -462,6 +462,10 @@ void free_plan(slm_plan* p) {
 
 }  // namespace
 
+// used by frames.hip
+int slm_set_error(int code, const char* msg) { return fail(code, "%s", msg); }
+int slm_current_device_ready() { return ensure_device(); }
+
 // ==========================================================================
 // C-ABI
 // ==========================================================================
