@@ -94,12 +94,12 @@ def targets(first: int, count: int, n: int) -> np.ndarray:
                      for b in range(first, first + count)])
 
 
-def kernel_roofline(plan, iters):
+def kernel_roofline(plan, iters, white_attention=0.0):
     """Time every launch of one run with HIP events on the plan's stream and
     price the dominant kernel class with its algorithmic bytes."""
-    us, cnt = plan.run_timed(iters)
+    us, cnt = plan.run_timed(iters, white_attention=white_attention)
     rows = {}
-    for cls in (_lib.KERNEL_COL_MAIN, _lib.KERNEL_ROW_MAIN):
+    for cls in (_lib.KERNEL_COL_MAIN, _lib.KERNEL_ROW_MAIN, _lib.KERNEL_GD_STATS):
         if cnt[cls] == 0:
             continue
         avg_us = us[cls] / cnt[cls]
@@ -156,25 +156,36 @@ def pcie_inclusive(plan, host_targets, iters, reps=5):
             "includes": "target upload + relayout, run, phase download (pageable host memory)"}
 
 
-def secondary(n, batch, iters):
+def secondary(n, batch, iters, algo=_lib.ALGO_GS, precision=None, reps=3):
     """Extra single-GPU measurements: one-run wall time and the per-kernel
-    roofline of another shape (4096^2 HBM stress, batched 1024^2)."""
+    roofline of another configuration (4096^2 HBM stress, batched 1024^2, GD,
+    float32 butterflies)."""
     t = targets(0, batch, n)
-    with _lib.Plan(_lib.ALGO_GS, batch, n, n, _lib.TGT_F32, False, iters) as plan:
+    with _lib.Plan(algo, batch, n, n, _lib.TGT_F32, False, iters) as plan:
         plan.set_target(t)
-        plan.run(iters)
+        if precision is not None:
+            plan.set_precision(precision)
+        wa = 0.0
+        if algo == _lib.ALGO_GD:  # BASELINE.json configs[2]: lr 0.005, white_attention 1, random guess seed 42
+            from spatial_light_modulator_module_amd import algorithms as alg
+
+            plan.set_lr(np.full(iters, 0.005, np.float32))
+            plan.set_field(np.stack([alg.make_initial_guess("random", None, t[k], 42) for k in range(batch)]))
+            wa = 1.0
+        plan.run(iters, white_attention=wa)
         plan.sync()
-        reps = 3
         t0 = time.perf_counter()
         for _ in range(reps):
-            plan.run(iters)
+            plan.run(iters, white_attention=wa)
         plan.sync()
         wall = (time.perf_counter() - t0) / reps
-        dom, rows, _, _ = kernel_roofline(plan, iters)
+        dom, rows, _, _ = kernel_roofline(plan, iters, wa)
         info = plan.info()
-    gs_iter_ms = wall / iters * 1e3
-    return {"shape": [batch, n, n], "iters": iters, "holograms_per_s": batch / wall, "gs_iter_ms": gs_iter_ms,
-            "gs_iter_ms_per_hologram": gs_iter_ms / batch, "kernels": rows, "dominant": dom, "tiling": info}
+    iter_ms = wall / iters * 1e3
+    return {"algo": "gd" if algo == _lib.ALGO_GD else "gs", "shape": [batch, n, n], "iters": iters,
+            "holograms_per_s": batch / wall, "iter_ms": iter_ms, "iter_ms_per_hologram": iter_ms / batch,
+            "kernels": rows, "dominant": dom,
+            "dominant_frac_of_hbm_peak": round(rows[dom]["achieved_gbs"] / HBM_PEAK_GBS, 4), "tiling": info}
 
 
 def main():
@@ -252,6 +263,11 @@ def main():
         try:
             extra["gs_4096"] = secondary(4096, 1, 20)
             extra["gs_1024_batch64"] = secondary(1024, 64, 20)
+            extra["gd_1024"] = secondary(1024, 1, 500, algo=_lib.ALGO_GD, reps=2)  # configs[2]
+            f32 = _lib.PRECISION_F32  # float32 butterflies (parity 2.4e-6..5.3e-6 at the 8c gates)
+            extra["f32_gs_1024"] = secondary(1024, 1, 200, precision=f32)
+            extra["f32_gs_4096"] = secondary(4096, 1, 20, precision=f32)
+            extra["f32_gs_1024_batch64"] = secondary(1024, 64, 20, precision=f32)
         except _lib.SlmError as e:  # pragma: no cover - report, do not hide
             extra["error"] = str(e)
         out["extra"] = extra

@@ -65,6 +65,7 @@ _SIGNATURES = [
     ("slm_plan_read_target_stats", _c_int, [_vp, _vp, _vp]),
     ("slm_plan_kernel_bytes", ctypes.c_longlong, [_vp, _c_int]),
     ("slm_plan_info", _c_int, [_vp, _vp]),
+    ("slm_plan_read_trace", _c_int, [_vp, _c_int, _vp]),
     ("slm_gs", _c_int, [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_double, _vp, _vp, _vp, _vp, _vp]),
     ("slm_gd", _c_int,
      [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_double, _vp, _vp, _c_float, _vp, _vp, _vp, _vp]),
@@ -267,6 +268,16 @@ class Plan:
         return {"col_cw": int(a[0]), "col_workgroups": int(a[1]), "col_threads": int(a[2]),
                 "row_threads": int(a[3]), "rows_per_workgroup": int(a[4]), "row_plan": int(a[5]),
                 "col_plan": int(a[6]), "precision": "f64" if a[7] == PRECISION_F64 else "f32"}
+
+    def read_trace(self, cls: int) -> np.ndarray:
+        """[batch * workgroups, 4] phase timestamps of the last launch of a
+        kernel class (SLM_TRACE builds with SLM_TRACE_BUF=1; diagnostics)."""
+        b, h, w = self.shape
+        info = self.info()
+        n = info["col_workgroups"] if cls == KERNEL_COL_MAIN else h // info["rows_per_workgroup"]
+        out = np.zeros((b * n, 4), np.uint64)
+        check(self._lib.slm_plan_read_trace(self.handle, cls, ptr(out)), "slm_plan_read_trace")
+        return out
 
     def gather_phase(self, counts, root: int = 0, host_out: np.ndarray | None = None) -> None:
         c = np.ascontiguousarray(counts, dtype=np.int32)

@@ -46,6 +46,7 @@ struct RowParams {
     long long holo;          // elements per hologram (H * W)
     float inv_s;             // 1 / (H * W)
     const void* tw;          // twiddle table for length W (float2 or double2)
+    unsigned long long* trace;  // SLM_TRACE builds: [workgroup][4] phase timestamps
 };
 
 struct ColParams {
@@ -66,6 +67,7 @@ struct ColParams {
     long long holo;          // elements per hologram
     float wa;                // GD white_attention
     const void* tw;          // twiddle table for length H (float2 or double2)
+    unsigned long long* trace;  // SLM_TRACE builds: [workgroup][4] phase timestamps
 };
 
 enum RowMode : int {
@@ -131,6 +133,24 @@ struct ColCfg {
     static constexpr bool kValid =
         THREADS >= 64 && THREADS <= 1024 && lds_line(PlanOf<K>::N) * CW * 8 <= 160 * 1024;
 };
+
+// Phase timeline of one workgroup (SLM_TRACE diagnostic builds only):
+// s_memrealtime (100 MHz, chip-wide) at entry, loads complete, transforms
+// done, stores complete.
+#ifndef SLM_TRACE
+#define SLM_TRACE 0
+#endif
+__device__ __forceinline__ void trace_point(unsigned long long* tr, long long wgid, int i, bool drain) {
+#if SLM_TRACE
+    if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (tr && threadIdx.x == 0) tr[wgid * 4 + i] = __builtin_amdgcn_s_memrealtime();
+#else
+    (void)tr;
+    (void)wgid;
+    (void)i;
+    (void)drain;
+#endif
+}
 
 // Waves per SIMD that the LDS footprint of a workgroup allows, handed to the
 // compiler as amdgpu_waves_per_eu (second __launch_bounds__ argument) so that
@@ -228,13 +248,30 @@ using CplxOf = std::conditional_t<P == 0, float2, double2>;
 #endif
 // float64 exchanges: narrow plans (more passes, hence more exchange roundings,
 // used for single small images where LDS is plentiful) and SLM_F64_XCHG builds
+// Narrow plans up to this length exchange in float64. Longer ones exchange in
+// complex64: half the LDS traffic, measured -2.5 % (1024^2) / -9 % (768x1024)
+// per iteration for warm-start parity 1.2e-6 instead of 4.3e-7 at 1024^2.
+#ifndef SLM_NARROW_F64_XCHG_MAX
+#define SLM_NARROW_F64_XCHG_MAX 512
+#endif
 template <int P, long long SLOTS, int K>
-using XchgOf = std::conditional_t<((SLM_F64_XCHG || kPlans[K].variant == 1) && P == 1 && SLOTS * 16 <= 80 * 1024),
+using XchgOf = std::conditional_t<((SLM_F64_XCHG || (kPlans[K].variant == 1 && kPlans[K].n <= SLM_NARROW_F64_XCHG_MAX)) &&
+                                   P == 1 && SLOTS * 16 <= 80 * 1024),
                                   double2, float2>;
 
+// float64: every twiddle of the thread cached in registers (loaded once per
+// kernel, behind the field loads, shared by both transforms) when they fit in
+// SLM_F64_TWCACHE_MAX VGPRs (the narrow single-image plans), so no pass waits
+// on a table load; otherwise read where used.
+#ifndef SLM_F64_TWCACHE_MAX
+#define SLM_F64_TWCACHE_MAX 0  // measured neutral at 1024^2 (80 caches the narrow plans)
+#endif
 template <int P, int THREADS, int K>
 constexpr int tw_mode() {
-    return P == 1 ? SLM_F64_TW : (THREADS <= 512 && PlanOf<K>::E <= 16 ? TW_CACHED : TW_DIRECT);
+    if constexpr (P == 1)
+        return TwCountOf<K, RadicesOf<K>>::value * 4 <= SLM_F64_TWCACHE_MAX && THREADS <= 512 ? TW_CACHED
+                                                                                             : SLM_F64_TW;
+    return THREADS <= 512 && PlanOf<K>::E <= 16 ? TW_CACHED : TW_DIRECT;
 }
 
 template <int TT>
@@ -329,6 +366,10 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
     const long long boff = hoff + blk_index(row, t, p.H);        // blocked (state), slot m adds m*T*H
     const long long bstep = (long long)T * p.H;
     const LdsLine<X> lds{smem + lrow * LINE};
+    // timeline of the iteration launches only (SLM_TRACE)
+    unsigned long long* const trace = (MODE == ROW_GS_MAIN || MODE == ROW_GD_MAIN) ? p.trace : nullptr;
+    const long long trace_id = (long long)b * gridDim.x + blockIdx.x;
+    trace_point(trace, trace_id, 0, false);
     Twiddles<K, C, tw_mode<P, RowCfg<K>::THREADS, K>()> tw;
     load_twiddles<K, C>(tw, t, p.tw);
     V v[E];
@@ -360,6 +401,7 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
         if (p.iter > p.stop_iter[b]) return;
     }
 
+    trace_point(trace, trace_id, 1, true);
     if constexpr (MODE == ROW_GS_PHASE) {
         fft_line_epi<K, true, C>(v, t, tw, lds, [&](int m, C& z) {
             p.phase_out[hoff + roff + t + T * m] = (float)atan2(z.y, z.x);
@@ -402,8 +444,10 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
             z = normalize(from_c64<C>(xs), a);
         });
     }
+    trace_point(trace, trace_id, 2, false);
 #pragma unroll
     for (int m = 0; m < E; ++m) store_field(p.out + boff + m * bstep, cv<float2>(v[m]), p.wt);
+    trace_point(trace, trace_id, 3, true);
 }
 
 // ------------------------------------------------------------------------
@@ -437,6 +481,9 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
     const long long base = (long long)b * p.holo + blk_index(t, x, H);
     constexpr long long kStep = 4LL * T;
     const LdsTile<CW, X> lds{smem, c};
+    unsigned long long* const trace = (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD) ? p.trace : nullptr;
+    const long long trace_id = (long long)b * gridDim.x + blockIdx.x;
+    trace_point(trace, trace_id, 0, false);
     Twiddles<K, C, tw_mode<P, THREADS, K>()> tw;
     load_twiddles<K, C>(tw, t, p.tw);
     V v[E];
@@ -483,6 +530,7 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
         if (p.iter > p.stop_iter[b]) return;
     }
 
+    trace_point(trace, trace_id, 1, true);
     if constexpr (MODE == COL_REAL_INV || MODE == COL_FFT_INV || MODE == COL_FFT_FWD) {
         fft_line<K, MODE != COL_FFT_FWD, C>(v, t, tw, lds);
 #pragma unroll
@@ -529,10 +577,12 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
                 dst[3] = 0.0;
             }
         }
+        trace_point(trace, trace_id, 2, false);
         if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD) {
 #pragma unroll
             for (int m = 0; m < E; ++m) store_field(p.out + base + m * kStep, cv<float2>(v[m]), p.wt);
         }
+        trace_point(trace, trace_id, 3, true);
     }
 }
 

@@ -185,6 +185,8 @@ struct slm_plan {
     hipStream_t stream = nullptr;
     int prec = PREC_F64;
     int wt = 1;  // write-through field stores ($SLM_WT=0 disables)
+    unsigned long long* trace_col = nullptr;  // SLM_TRACE diagnostics ($SLM_TRACE_BUF=1)
+    unsigned long long* trace_row = nullptr;
     const void* tw_row = nullptr;
     const void* tw_col = nullptr;
     float2 *xa = nullptr, *xb = nullptr, *y = nullptr, *field = nullptr;
@@ -289,6 +291,7 @@ RowParams row_params(slm_plan* p) {
     r.inv_s = (float)(1.0 / (double)p->holo);
     r.tw = p->tw_row;
     r.wt = p->wt;
+    r.trace = p->trace_row;
     return r;
 }
 
@@ -305,6 +308,7 @@ ColParams col_params(slm_plan* p) {
     c.holo = p->holo;
     c.tw = p->tw_col;
     c.wt = p->wt;
+    c.trace = p->trace_col;
     return c;
 }
 
@@ -450,7 +454,8 @@ void free_plan(slm_plan* p) {
     for (void* ptr : {(void*)p->xa, (void*)p->xb, (void*)p->y, (void*)p->field, p->tgt, (void*)p->ain,
                       (void*)p->phase_in, (void*)p->phase_out, (void*)p->e_out, (void*)p->partials,
                       (void*)p->stats, (void*)p->stop, (void*)p->norm, (void*)p->normf, (void*)p->sum_t2,
-                      (void*)p->ts_part, (void*)p->lr, (void*)p->gather_buf})
+                      (void*)p->ts_part, (void*)p->lr, (void*)p->gather_buf, (void*)p->trace_col,
+                      (void*)p->trace_row})
         if (ptr) (void)hipFree(ptr);
     for (auto& e : p->ev_pool) {
         (void)hipEventDestroy(e.first);
@@ -570,7 +575,22 @@ int slm_plan_create(int algo, int batch, int height, int width, int tgt_type, in
     RC(alloc((void**)&p->normf, (size_t)batch * sizeof(float)));
     RC(alloc((void**)&p->sum_t2, (size_t)batch * sizeof(double)));
     RC(alloc((void**)&p->ts_part, (size_t)batch * kTsBlocks * 2 * sizeof(double)));
+    if (const char* e = std::getenv("SLM_TRACE_BUF"); e && std::atoi(e)) {
+        RC(alloc((void**)&p->trace_col, (size_t)batch * p->nwg * 4 * sizeof(unsigned long long)));
+        RC(alloc((void**)&p->trace_row, (size_t)batch * (height / p->rpw) * 4 * sizeof(unsigned long long)));
+    }
     *out = p;
+    return 0;
+}
+
+int slm_plan_read_trace(slm_plan* p, int kernel_class, unsigned long long* out) {
+    if (!p || !out) return fail(SLM_ERR_ARG, "null argument");
+    unsigned long long* src = kernel_class == SLM_KERNEL_COL_MAIN ? p->trace_col
+                              : kernel_class == SLM_KERNEL_ROW_MAIN ? p->trace_row : nullptr;
+    if (!src) return fail(SLM_ERR_STATE, "no trace buffer (set SLM_TRACE_BUF=1 before creating the plan)");
+    const long long n = (long long)p->B * (kernel_class == SLM_KERNEL_COL_MAIN ? p->nwg : p->H / p->rpw) * 4;
+    HIP_TRY(hipStreamSynchronize(p->stream));
+    HIP_TRY(hipMemcpy(out, src, n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     return 0;
 }
 

@@ -21,5 +21,5 @@ for k in "$@"; do
   pids="$pids $!"
 done
 for p in $pids; do wait $p; done
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $root/spatial_light_modulator_module_amd/lib/libslm_hip_$name.so $objs $base/slm_capi.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $root/spatial_light_modulator_module_amd/lib/libslm_hip_$name.so $objs $base/slm_capi.o $base/frames.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 echo built libslm_hip_$name.so
