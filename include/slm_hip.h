@@ -39,8 +39,8 @@ extern "C" {
 #define SLM_TGT_F32 1 /* float32 target; amplitude = sqrtf(T) */
 
 /* arithmetic precision of the transforms (state is complex64 in HBM either way) */
-#define SLM_PRECISION_F32 0 /* float32 butterflies and twiddles */
-#define SLM_PRECISION_F64 1 /* float64 butterflies and twiddles (default; $SLM_PRECISION=f32 overrides) */
+#define SLM_PRECISION_F32 0 /* float32 butterflies and twiddles (default; $SLM_PRECISION=f64 overrides) */
+#define SLM_PRECISION_F64 1 /* float64 butterflies and twiddles */
 
 /* kernel classes for timing / roofline queries */
 #define SLM_KERNEL_COL_MAIN 0 /* GS column pass, or GD gradient column pass */

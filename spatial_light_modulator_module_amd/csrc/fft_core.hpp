@@ -449,13 +449,17 @@ __device__ __forceinline__ void load_twiddles(Twiddles<N, C, MODE>& tw, int t, c
 // the exchange's ds_reads below the following barrier, so a fast wave's next
 // pass overwrote LDS a slow wave had not read yet (a ~1.5 % per-launch race).
 // The memory clobbers and sched_barrier pin every LDS access to its side.
-__device__ __forceinline__ void exchange_barrier() {
+// The barrier waits for this wave's LDS operations only (lgkmcnt), never for
+// vector memory: __syncthreads()' workgroup fence may drain vmcnt, which would
+// stall on loads issued for the next tile (kernels.hpp, tile_loop).
+__device__ __forceinline__ void lds_barrier() {
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
 }
+__device__ __forceinline__ void exchange_barrier() { lds_barrier(); }
 
 // ------------------------------------------------------------------------
 // Stockham driver.

@@ -46,7 +46,9 @@ struct RowParams {
     long long holo;          // elements per hologram (H * W)
     float inv_s;             // 1 / (H * W)
     const void* tw;          // twiddle table for length W (float2 or double2)
-    unsigned long long* trace;  // SLM_TRACE builds: [workgroup][4] phase timestamps
+    unsigned long long* trace;  // SLM_TRACE builds: [tile][4] phase timestamps
+    int B;                   // holograms
+    int ntile;               // row groups per hologram (H / rows per workgroup)
 };
 
 struct ColParams {
@@ -67,7 +69,8 @@ struct ColParams {
     long long holo;          // elements per hologram
     float wa;                // GD white_attention
     const void* tw;          // twiddle table for length H (float2 or double2)
-    unsigned long long* trace;  // SLM_TRACE builds: [workgroup][4] phase timestamps
+    unsigned long long* trace;  // SLM_TRACE builds: [tile][4] phase timestamps
+    int B;                   // holograms
 };
 
 enum RowMode : int {
@@ -120,8 +123,15 @@ struct RowCfg {
     // or a row pair when a quad would not leave room for two workgroups per CU
     // and a pair still fills 8 waves (the partner pair, which reads the other
     // half of each 128-B line, is placed on the same XCD: row_kernel remap)
-    static constexpr bool kPairs = 4 * PlanOf<K>::ROWSTRIDE * 8 > kLdsPair && (SLM_ROW_PAIRS || T >= 256);
+    // Narrow plans (single small images: few workgroups per CU) always use
+    // pairs: twice the workgroups, measured 11.6 -> 9.1 us per 1024^2 row pass.
+    static constexpr bool kPairs = (4 * PlanOf<K>::ROWSTRIDE * 8 > kLdsPair && (SLM_ROW_PAIRS || T >= 256)) ||
+                                   kPlans[K].variant == 1;
+#ifdef SLM_ROW_RPW
+    static constexpr int RPW = (T >= 64) ? SLM_ROW_RPW : 256 / T;
+#else
     static constexpr int RPW = (T >= 64) ? (kPairs ? 2 : 4) : 256 / T;
+#endif
     static constexpr int QR = RPW < 4 ? RPW : 4;  // rows interleaved across a wave
     static constexpr int THREADS = RPW * T;
 };
@@ -235,6 +245,18 @@ __device__ __forceinline__ void store_field(float2* dst, float2 v, int wt) {
         *dst = v;
 }
 
+#ifndef SLM_PREFETCH
+#define SLM_PREFETCH 0  // measured: no gain over one tile per workgroup (the transforms, not the loads, bound a tile)
+#endif
+// Persistent (looping, prefetching) kernels: float32 compute with at most 16
+// elements per thread, where the next tile's complex64 slots fit in registers
+// beside the current ones (-DSLM_PREFETCH=1 builds; twiddles as for one tile).
+// Every other kernel runs one tile per workgroup (grid = tiles). The host
+// sizes grids with the same predicate (slm_capi.hip, tile_grid).
+__host__ __device__ constexpr bool tile_persistent(int prec, int e) {
+    return SLM_PREFETCH && prec == PREC_F32 && e <= 16;
+}
+
 template <int P>
 using CplxOf = std::conditional_t<P == 0, float2, double2>;
 
@@ -271,7 +293,11 @@ constexpr int tw_mode() {
     if constexpr (P == 1)
         return TwCountOf<K, RadicesOf<K>>::value * 4 <= SLM_F64_TWCACHE_MAX && THREADS <= 512 ? TW_CACHED
                                                                                              : SLM_F64_TW;
+#ifdef SLM_F32_TW
+    return SLM_F32_TW;
+#else
     return THREADS <= 512 && PlanOf<K>::E <= 16 ? TW_CACHED : TW_DIRECT;
+#endif
 }
 
 template <int TT>
@@ -308,7 +334,7 @@ __device__ __forceinline__ void block_reduce_stats(double& mx, double& s2, doubl
             red[wid][1] = s2;
             red[wid][2] = st;
         }
-        __syncthreads();
+        lds_barrier();
         if (threadIdx.x == 0) {
             for (int w = 1; w < NW; ++w) {
                 mx = fmax(mx, red[w][0]);
@@ -323,6 +349,45 @@ __device__ __forceinline__ void block_reduce_stats(double& mx, double& s2, doubl
 // fft_core.hpp, Stockham driver), else the compute type
 template <int P, class X>
 using StateOf = std::conditional_t<std::is_same_v<X, float2>, float2, CplxOf<P>>;
+
+// ------------------------------------------------------------------------
+// persistent tile loop (both passes)
+// ------------------------------------------------------------------------
+// A launch covers `total` tiles (column panels or row groups of every
+// hologram) with G = gridDim.x <= total workgroups, G at most what the chip
+// holds at once (host: tile_grid). Workgroup w takes tiles lid(w), lid(w) + G,
+// ... where lid is the XCD-aware remap, so within one round the workgroups of
+// an XCD hold neighbouring tiles. The next tile's inputs are loaded into
+// registers before the current tile is transformed (kPrefetch), so their HBM
+// latency hides behind the transforms and the current tile's stores; the LDS
+// barriers never wait for vector memory (lds_barrier), so the loads stay in
+// flight across them.
+template <bool PERSIST, int NT, class LoadF, class ProcF, class V, int E>
+__device__ __forceinline__ void tile_loop(long long total, LoadF&& load, ProcF&& process, V (&v)[E],
+                                          float (&tv)[NT]) {
+    const int G = gridDim.x;
+    long long tile = xcd_remap(blockIdx.x, G);
+    if (tile >= total) return;
+    load(tile, v, tv);
+    if constexpr (!PERSIST) {
+        process(tile, v, tv);
+    } else {
+        for (;;) {
+            const long long next = tile + G;
+            const bool more = next < total;
+            V vn[E];
+            float tn[NT];
+            if (more) load(next, vn, tn);
+            process(tile, v, tv);
+            if (!more) break;
+#pragma unroll
+            for (int m = 0; m < E; ++m) v[m] = vn[m];
+#pragma unroll
+            for (int m = 0; m < NT; ++m) tv[m] = tn[m];
+            tile = next;
+        }
+    }
+}
 
 // ------------------------------------------------------------------------
 // row pass
@@ -347,7 +412,6 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
     using V = StateOf<P, X>;
     __shared__ X smem[RPW * LINE];
 
-    const int b = blockIdx.y;
     // lane -> (row within the quad, transform thread t): TL consecutive t of
     // one row, then the next row of the quad. One wave instruction touches
     // 16 consecutive x of 4 rows = four whole 128-B lines of the blocked layout,
@@ -359,95 +423,107 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
     const int qq = rest / (T / TL);
     const int t = tlo + TL * (rest - qq * (T / TL));
     const int lrow = qq * QR + q4;
-    // consecutive row groups on one XCD (row pairs share 128-B lines through its L2)
-    const int row = xcd_remap(blockIdx.x, gridDim.x) * RPW + lrow;
-    const long long hoff = (long long)b * p.holo;
-    const long long roff = (long long)row * W;                  // row-major (user arrays)
-    const long long boff = hoff + blk_index(row, t, p.H);        // blocked (state), slot m adds m*T*H
-    const long long bstep = (long long)T * p.H;
+    const long long bstep = (long long)T * p.H;  // slot m adds m * bstep (blocked layout)
     const LdsLine<X> lds{smem + lrow * LINE};
-    // timeline of the iteration launches only (SLM_TRACE)
-    unsigned long long* const trace = (MODE == ROW_GS_MAIN || MODE == ROW_GD_MAIN) ? p.trace : nullptr;
-    const long long trace_id = (long long)b * gridDim.x + blockIdx.x;
-    trace_point(trace, trace_id, 0, false);
     Twiddles<K, C, tw_mode<P, RowCfg<K>::THREADS, K>()> tw;
     load_twiddles<K, C>(tw, t, p.tw);
-    V v[E];
 
-    auto ain_at = [&](int m) -> S { return p.ain ? (S)p.ain[roff + t + T * m] : (S)1; };
-
-    if constexpr (MODE == ROW_PHASE_FWD) {
+    // tile = (hologram b, row group g); rows g * RPW + lrow
+    auto where = [&](long long tile, int& b, long long& hoff, long long& roff, long long& boff) {
+        b = (int)(tile / p.ntile);
+        const int row = (int)(tile - (long long)b * p.ntile) * RPW + lrow;
+        hoff = (long long)b * p.holo;
+        roff = (long long)row * W;                  // row-major (user arrays)
+        boff = hoff + blk_index(row, t, p.H);       // blocked (state)
+    };
+    auto load = [&](long long tile, V (&v)[E], float (&)[1]) {
+        int b;
+        long long hoff, roff, boff;
+        where(tile, b, hoff, roff, boff);
+        auto ain_at = [&](int m) -> S { return p.ain ? (S)p.ain[roff + t + T * m] : (S)1; };
+        if constexpr (MODE == ROW_PHASE_FWD) {
 #pragma unroll
-        for (int m = 0; m < E; ++m) {
-            S sn, cs;
-            if constexpr (P == 0)
-                sincosf(p.phase_in[hoff + roff + t + T * m], &sn, &cs);
-            else
-                sincos((double)p.phase_in[hoff + roff + t + T * m], &sn, &cs);
-            const S a = ain_at(m);
-            v[m] = cv<V>(mk<C>(a * cs, a * sn));
+            for (int m = 0; m < E; ++m) {
+                S sn, cs;
+                if constexpr (P == 0)
+                    sincosf(p.phase_in[hoff + roff + t + T * m], &sn, &cs);
+                else
+                    sincos((double)p.phase_in[hoff + roff + t + T * m], &sn, &cs);
+                const S a = ain_at(m);
+                v[m] = cv<V>(mk<C>(a * cs, a * sn));
+            }
+        } else if constexpr (MODE == ROW_GD_INIT_FIELD) {
+#pragma unroll
+            for (int m = 0; m < E; ++m) v[m] = cv<V>(normalize(from_c64<C>(p.field[boff + m * bstep]), ain_at(m)));
+        } else {
+#pragma unroll
+            for (int m = 0; m < E; ++m) v[m] = cv<V>(p.in[boff + m * bstep]);
         }
-    } else if constexpr (MODE == ROW_GD_INIT_FIELD) {
+    };
+    auto process = [&](long long tile, V (&v)[E], float (&)[1]) {
+        int b;
+        long long hoff, roff, boff;
+        where(tile, b, hoff, roff, boff);
+        auto ain_at = [&](int m) -> S { return p.ain ? (S)p.ain[roff + t + T * m] : (S)1; };
+        // timeline of the iteration launches only (SLM_TRACE)
+        unsigned long long* const trace = (MODE == ROW_GS_MAIN || MODE == ROW_GD_MAIN) ? p.trace : nullptr;
+        trace_point(trace, tile, 0, false);
+        if constexpr (MODE == ROW_GS_MAIN) {
+            if (p.iter >= p.stop_iter[b]) return;  // stopped after this iteration's column pass
+        } else if constexpr (MODE == ROW_GD_MAIN) {
+            if (p.iter > p.stop_iter[b]) return;
+        }
+        trace_point(trace, tile, 1, true);
+        if constexpr (MODE == ROW_GS_PHASE) {
+            fft_line_epi<K, true, C>(v, t, tw, lds, [&](int m, C& z) {
+                p.phase_out[hoff + roff + t + T * m] = (float)atan2(z.y, z.x);
+            });
+            return;
+        } else if constexpr (MODE == ROW_FFT_INV || MODE == ROW_FFT_FWD) {
+            fft_line<K, MODE == ROW_FFT_INV, C>(v, t, tw, lds);
+        } else if constexpr (MODE == ROW_PHASE_FWD || MODE == ROW_GD_INIT_FIELD) {
+            fft_line<K, false, C>(v, t, tw, lds);
+        } else if constexpr (MODE == ROW_GS_MAIN) {
+            // A -> B = a_in A/|A| (src/algorithms.py:30)
+            fft_pair<K, true, false, C>(v, t, tw, lds, [&](int m, C& z) { z = unit_scale(z, ain_at(m)); });
+        } else if constexpr (MODE == ROW_GD_INIT_Y) {
+            fft_pair<K, true, false, C>(v, t, tw, lds, [&](int m, C& z) {
+                const S a = ain_at(m);
+                const C x = unit_scale(z, a);  // a_in exp(i angle(ifft2(sqrt T)))
+                p.field[boff + m * bstep] = to_c64(x);
+                z = normalize(x, a);
+            });
+        } else if constexpr (MODE == ROW_GD_MAIN) {
+            // dEdF = ifft2(...) * a_in (src/algorithms.py:87-89); dEdX_complex (:179-185);
+            // input -= lr * dEdX (:91); next forward input x/|x| a_in (:84).
+            const S lr = (S)p.lr[p.iter];
+            const S inv_s = (S)1 / (S)p.holo;
+            fft_pair<K, true, false, C>(v, t, tw, lds, [&](int m, C& z) {
+                const S a = ain_at(m);
+                const C g = mk<C>(z.x * inv_s * a, z.y * inv_s * a);
+                const long long idx = boff + m * bstep;
+                C x = from_c64<C>(p.field[idx]);
+                const S ax2 = x.x * x.x + x.y * x.y;
+                const S inv = rsqrt_nr(ax2);
+                const S inv3 = inv * inv * inv;
+                const S re = x.x * g.x + x.y * g.y;
+                const S dx = g.x * inv - x.x * re * inv3;
+                const S dy = g.y * inv - x.y * re * inv3;
+                x.x -= lr * dx;
+                x.y -= lr * dy;
+                const float2 xs = to_c64(x);  // the field is stored in complex64
+                p.field[idx] = xs;
+                z = normalize(from_c64<C>(xs), a);
+            });
+        }
+        trace_point(trace, tile, 2, false);
 #pragma unroll
-        for (int m = 0; m < E; ++m) v[m] = cv<V>(normalize(from_c64<C>(p.field[boff + m * bstep]), ain_at(m)));
-    } else {
-#pragma unroll
-        for (int m = 0; m < E; ++m) v[m] = cv<V>(p.in[boff + m * bstep]);
-    }
-    // the stop test is issued behind the loads so its latency overlaps them
-    if constexpr (MODE == ROW_GS_MAIN) {
-        if (p.iter >= p.stop_iter[b]) return;  // stopped after this iteration's column pass
-    } else if constexpr (MODE == ROW_GD_MAIN) {
-        if (p.iter > p.stop_iter[b]) return;
-    }
-
-    trace_point(trace, trace_id, 1, true);
-    if constexpr (MODE == ROW_GS_PHASE) {
-        fft_line_epi<K, true, C>(v, t, tw, lds, [&](int m, C& z) {
-            p.phase_out[hoff + roff + t + T * m] = (float)atan2(z.y, z.x);
-        });
-        return;
-    } else if constexpr (MODE == ROW_FFT_INV || MODE == ROW_FFT_FWD) {
-        fft_line<K, MODE == ROW_FFT_INV, C>(v, t, tw, lds);
-    } else if constexpr (MODE == ROW_PHASE_FWD || MODE == ROW_GD_INIT_FIELD) {
-        fft_line<K, false, C>(v, t, tw, lds);
-    } else if constexpr (MODE == ROW_GS_MAIN) {
-        // A -> B = a_in A/|A| (src/algorithms.py:30)
-        fft_pair<K, true, false, C>(v, t, tw, lds, [&](int m, C& z) { z = unit_scale(z, ain_at(m)); });
-    } else if constexpr (MODE == ROW_GD_INIT_Y) {
-        fft_pair<K, true, false, C>(v, t, tw, lds, [&](int m, C& z) {
-            const S a = ain_at(m);
-            const C x = unit_scale(z, a);  // a_in exp(i angle(ifft2(sqrt T)))
-            p.field[boff + m * bstep] = to_c64(x);
-            z = normalize(x, a);
-        });
-    } else if constexpr (MODE == ROW_GD_MAIN) {
-        // dEdF = ifft2(...) * a_in (src/algorithms.py:87-89); dEdX_complex (:179-185);
-        // input -= lr * dEdX (:91); next forward input x/|x| a_in (:84).
-        const S lr = (S)p.lr[p.iter];
-        const S inv_s = (S)1 / (S)p.holo;
-        fft_pair<K, true, false, C>(v, t, tw, lds, [&](int m, C& z) {
-            const S a = ain_at(m);
-            const C g = mk<C>(z.x * inv_s * a, z.y * inv_s * a);
-            const long long idx = boff + m * bstep;
-            C x = from_c64<C>(p.field[idx]);
-            const S ax2 = x.x * x.x + x.y * x.y;
-            const S inv = rsqrt_nr(ax2);
-            const S inv3 = inv * inv * inv;
-            const S re = x.x * g.x + x.y * g.y;
-            const S dx = g.x * inv - x.x * re * inv3;
-            const S dy = g.y * inv - x.y * re * inv3;
-            x.x -= lr * dx;
-            x.y -= lr * dy;
-            const float2 xs = to_c64(x);  // the field is stored in complex64
-            p.field[idx] = xs;
-            z = normalize(from_c64<C>(xs), a);
-        });
-    }
-    trace_point(trace, trace_id, 2, false);
-#pragma unroll
-    for (int m = 0; m < E; ++m) store_field(p.out + boff + m * bstep, cv<float2>(v[m]), p.wt);
-    trace_point(trace, trace_id, 3, true);
+        for (int m = 0; m < E; ++m) store_field(p.out + boff + m * bstep, cv<float2>(v[m]), p.wt);
+        trace_point(trace, tile, 3, true);
+    };
+    V v[E];
+    float none[1];
+    tile_loop<tile_persistent(P, E)>(p.ntile * (long long)p.B, load, process, v, none);
 }
 
 // ------------------------------------------------------------------------
@@ -472,118 +548,128 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
     using V = StateOf<P, X>;
     __shared__ X smem[LINE * CW];
 
-    const int b = blockIdx.y;
-    const int wg = xcd_remap(blockIdx.x, gridDim.x);
     const int c = threadIdx.x % CW;
     const int t = threadIdx.x / CW;
-    const int x = wg * CW + c;
-    // blocked layout: element (y, x) at blk_index(y, x, H); row y = t + T m
-    const long long base = (long long)b * p.holo + blk_index(t, x, H);
-    constexpr long long kStep = 4LL * T;
+    constexpr long long kStep = 4LL * T;  // blocked layout: row y = t + T m
     const LdsTile<CW, X> lds{smem, c};
-    unsigned long long* const trace = (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD) ? p.trace : nullptr;
-    const long long trace_id = (long long)b * gridDim.x + blockIdx.x;
-    trace_point(trace, trace_id, 0, false);
     Twiddles<K, C, tw_mode<P, THREADS, K>()> tw;
     load_twiddles<K, C>(tw, t, p.tw);
-    V v[E];
     constexpr bool kTarget = (MODE == COL_GS_MAIN || MODE == COL_GD_STATS || MODE == COL_GD_GRAD);
-    float tv[kTarget ? E : 1];
+    constexpr int NT = kTarget ? E : 1;
 
-    // GD gradient needs this iteration's global max of |F|^2 (src/algorithms.py:86).
-    S maxp = 0;
-    if constexpr (MODE == COL_GD_GRAD) {
-        __shared__ double smax;
-        const double* part = p.partials + ((long long)b * p.max_loops + p.iter) * p.nwg * 4;
-        double m = 0.0;
-        for (int k = threadIdx.x; k < p.nwg; k += THREADS) m = fmax(m, part[k * 4]);
-        double d1 = 0.0, d2 = 0.0;
-        block_reduce_stats<THREADS>(m, d1, d2);
-        if (threadIdx.x == 0) smax = m;
-        __syncthreads();
-        maxp = (S)smax;
-    }
-
-    if constexpr (MODE == COL_REAL_INV) {
+    // tile = (hologram b, column panel wg); element (y, x) at blk_index(y, x, H)
+    auto where = [&](long long tile, int& b, int& wg, long long& base) {
+        b = (int)(tile / p.nwg);
+        wg = (int)(tile - (long long)b * p.nwg);
+        base = (long long)b * p.holo + blk_index(t, wg * CW + c, H);
+    };
+    auto load = [&](long long tile, V (&v)[E], float (&tv)[NT]) {
+        int b, wg;
+        long long base;
+        where(tile, b, wg, base);
+        if constexpr (MODE == COL_REAL_INV) {
 #pragma unroll
-        for (int m = 0; m < E; ++m) {
-            const float a = TgtLoad<TT>::amp(TgtLoad<TT>::load(p.tgt, base + m * kStep));
-            v[m] = cv<V>(mk<C>((S)a, (S)0));
+            for (int m = 0; m < E; ++m) {
+                const float a = TgtLoad<TT>::amp(TgtLoad<TT>::load(p.tgt, base + m * kStep));
+                v[m] = cv<V>(mk<C>((S)a, (S)0));
+            }
+        } else if constexpr (MODE == COL_EXPECTED) {
+            // GD keeps X of iteration i in buffer i % 2; GS passes the same buffer twice.
+            const int s = min(p.stop_iter[b], p.loops - 1);
+            const float2* src = (s & 1) ? p.in_alt : p.in;
+#pragma unroll
+            for (int m = 0; m < E; ++m) v[m] = cv<V>(src[base + m * kStep]);
+        } else {
+#pragma unroll
+            for (int m = 0; m < E; ++m) v[m] = cv<V>(p.in[base + m * kStep]);
         }
-    } else if constexpr (MODE == COL_EXPECTED) {
-        // GD keeps X of iteration i in buffer i % 2; GS passes the same buffer twice.
-        const int s = min(p.stop_iter[b], p.loops - 1);
-        const float2* src = (s & 1) ? p.in_alt : p.in;
+        if constexpr (kTarget) {
+            // the target is consumed in the middle of the transforms: fetch it with the field
 #pragma unroll
-        for (int m = 0; m < E; ++m) v[m] = cv<V>(src[base + m * kStep]);
-    } else {
-#pragma unroll
-        for (int m = 0; m < E; ++m) v[m] = cv<V>(p.in[base + m * kStep]);
-    }
-    if constexpr (kTarget) {
-        // the target is consumed in the middle of the kernel: fetch it up front
-#pragma unroll
-        for (int m = 0; m < E; ++m) tv[m] = TgtLoad<TT>::load(p.tgt, base + m * kStep);
-    }
-    // the stop test is issued behind the loads so its latency overlaps them
-    if constexpr (kTarget) {
-        if (p.iter > p.stop_iter[b]) return;
-    }
-
-    trace_point(trace, trace_id, 1, true);
-    if constexpr (MODE == COL_REAL_INV || MODE == COL_FFT_INV || MODE == COL_FFT_FWD) {
-        fft_line<K, MODE != COL_FFT_FWD, C>(v, t, tw, lds);
-#pragma unroll
-        for (int m = 0; m < E; ++m) store_field(p.out + base + m * kStep, cv<float2>(v[m]), p.wt);
-        return;
-    } else if constexpr (MODE == COL_EXPECTED) {
-        const long long nat = (long long)b * p.holo + (long long)t * p.W + x;  // row-major output
-        fft_line_epi<K, false, C>(v, t, tw, lds, [&](int m, C& z) {
-            p.e_out[nat + (long long)m * T * p.W] = (float)(z.x * z.x + z.y * z.y);
-        });
-        return;
-    } else {
-        double mx = 0.0, s2 = 0.0, st = 0.0;
-        const S norm = (MODE == COL_GD_GRAD) ? (S)p.norm[b] : (S)0;
-        auto epi = [&](int m, C& z) {
-            const S e = z.x * z.x + z.y * z.y;
-            if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_STATS) {
-                // |C|^2 as the reference's float64 expected_outcome sees it
-                const double ed = (double)(float)e;
-                mx = fmax(mx, ed);
-                s2 += ed * ed;
-                st += ed * (double)tv[m];
-            }
-            if constexpr (MODE == COL_GS_MAIN) {
-                z = unit_scale(z, (S)TgtLoad<TT>::amp(tv[m]));  // D = a_T C/|C| (src/algorithms.py:33)
-            } else if constexpr (MODE == COL_GD_GRAD) {
-                // mask * F * (output - T), output = |F|^2 norm / max (src/algorithms.py:80,85-88)
-                const S o = e * norm / maxp;
-                const S w = ((S)1 + (S)p.wa * (S)tv[m] / (S)255) * (o - (S)tv[m]);
-                z = mk<C>(z.x * w, z.y * w);
-            }
-        };
-        if constexpr (MODE == COL_GD_STATS)
-            fft_line_epi<K, false, C>(v, t, tw, lds, epi);
-        else
-            fft_pair<K, false, true, C>(v, t, tw, lds, epi);
-        if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_STATS) {
-            block_reduce_stats<THREADS>(mx, s2, st);
-            if (threadIdx.x == 0) {
-                double* dst = p.partials + (((long long)b * p.max_loops + p.iter) * p.nwg + wg) * 4;
-                dst[0] = mx;
-                dst[1] = s2;
-                dst[2] = st;
-                dst[3] = 0.0;
-            }
+            for (int m = 0; m < E; ++m) tv[m] = TgtLoad<TT>::load(p.tgt, base + m * kStep);
         }
-        trace_point(trace, trace_id, 2, false);
-        if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD) {
+    };
+    auto process = [&](long long tile, V (&v)[E], float (&tv)[NT]) {
+        int b, wg;
+        long long base;
+        where(tile, b, wg, base);
+        const int x = wg * CW + c;
+        unsigned long long* const trace = (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD) ? p.trace : nullptr;
+        trace_point(trace, tile, 0, false);
+        if constexpr (kTarget) {
+            if (p.iter > p.stop_iter[b]) return;
+        }
+        // GD gradient needs this iteration's global max of |F|^2 (src/algorithms.py:86).
+        S maxp = 0;
+        if constexpr (MODE == COL_GD_GRAD) {
+            __shared__ double smax;
+            const double* part = p.partials + ((long long)b * p.max_loops + p.iter) * p.nwg * 4;
+            double m = 0.0;
+            for (int k = threadIdx.x; k < p.nwg; k += THREADS) m = fmax(m, part[k * 4]);
+            double d1 = 0.0, d2 = 0.0;
+            block_reduce_stats<THREADS>(m, d1, d2);
+            if (threadIdx.x == 0) smax = m;
+            lds_barrier();
+            maxp = (S)smax;
+        }
+        trace_point(trace, tile, 1, true);
+        if constexpr (MODE == COL_REAL_INV || MODE == COL_FFT_INV || MODE == COL_FFT_FWD) {
+            fft_line<K, MODE != COL_FFT_FWD, C>(v, t, tw, lds);
 #pragma unroll
             for (int m = 0; m < E; ++m) store_field(p.out + base + m * kStep, cv<float2>(v[m]), p.wt);
+            return;
+        } else if constexpr (MODE == COL_EXPECTED) {
+            const long long nat = (long long)b * p.holo + (long long)t * p.W + x;  // row-major output
+            fft_line_epi<K, false, C>(v, t, tw, lds, [&](int m, C& z) {
+                p.e_out[nat + (long long)m * T * p.W] = (float)(z.x * z.x + z.y * z.y);
+            });
+            return;
+        } else {
+            double mx = 0.0, s2 = 0.0, st = 0.0;
+            const S norm = (MODE == COL_GD_GRAD) ? (S)p.norm[b] : (S)0;
+            auto epi = [&](int m, C& z) {
+                const S e = z.x * z.x + z.y * z.y;
+                if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_STATS) {
+                    // |C|^2 as the reference's float64 expected_outcome sees it
+                    const double ed = (double)(float)e;
+                    mx = fmax(mx, ed);
+                    s2 += ed * ed;
+                    st += ed * (double)tv[m];
+                }
+                if constexpr (MODE == COL_GS_MAIN) {
+                    z = unit_scale(z, (S)TgtLoad<TT>::amp(tv[m]));  // D = a_T C/|C| (src/algorithms.py:33)
+                } else if constexpr (MODE == COL_GD_GRAD) {
+                    // mask * F * (output - T), output = |F|^2 norm / max (src/algorithms.py:80,85-88)
+                    const S o = e * norm / maxp;
+                    const S w = ((S)1 + (S)p.wa * (S)tv[m] / (S)255) * (o - (S)tv[m]);
+                    z = mk<C>(z.x * w, z.y * w);
+                }
+            };
+            if constexpr (MODE == COL_GD_STATS)
+                fft_line_epi<K, false, C>(v, t, tw, lds, epi);
+            else
+                fft_pair<K, false, true, C>(v, t, tw, lds, epi);
+            if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_STATS) {
+                block_reduce_stats<THREADS>(mx, s2, st);
+                if (threadIdx.x == 0) {
+                    double* dst = p.partials + (((long long)b * p.max_loops + p.iter) * p.nwg + wg) * 4;
+                    dst[0] = mx;
+                    dst[1] = s2;
+                    dst[2] = st;
+                    dst[3] = 0.0;
+                }
+            }
+            trace_point(trace, tile, 2, false);
+            if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD) {
+#pragma unroll
+                for (int m = 0; m < E; ++m) store_field(p.out + base + m * kStep, cv<float2>(v[m]), p.wt);
+            }
+            trace_point(trace, tile, 3, true);
         }
-        trace_point(trace, trace_id, 3, true);
-    }
+    };
+    V v[E];
+    float tv[NT];
+    tile_loop<tile_persistent(P, E)>(p.nwg * (long long)p.B, load, process, v, tv);
 }
 
 // ------------------------------------------------------------------------

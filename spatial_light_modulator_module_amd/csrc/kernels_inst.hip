@@ -55,6 +55,7 @@ ColFn col_table_cw(int mode, int tt) {
 template <int N, int P>
 ColFn col_table(int cw, int mode, int tt) {
     switch (cw) {
+        case 1: return col_table_cw<N, 1, P>(mode, tt);
         case 2: return col_table_cw<N, 2, P>(mode, tt);
         case 4: return col_table_cw<N, 4, P>(mode, tt);
         case 8: return col_table_cw<N, 8, P>(mode, tt);

@@ -183,7 +183,7 @@ struct slm_plan {
     int device = 0;
     long long holo = 0;
     hipStream_t stream = nullptr;
-    int prec = PREC_F64;
+    int prec = PREC_F32;  // butterflies/twiddles; parity at both precisions: tests/test_gpu_precision.py
     int wt = 1;  // write-through field stores ($SLM_WT=0 disables)
     unsigned long long* trace_col = nullptr;  // SLM_TRACE diagnostics ($SLM_TRACE_BUF=1)
     unsigned long long* trace_row = nullptr;
@@ -215,6 +215,12 @@ struct slm_plan {
 
 namespace {
 
+#define RC(x)                 \
+    do {                      \
+        int rc_ = (x);        \
+        if (rc_) return rc_;  \
+    } while (0)
+
 // Column tile width. With the blocked state layout a 4-column panel is one
 // contiguous run, so a 4-column tile moves whole lines (2-column tiles, which
 // rely on the partner tile fetching the other half of each line through the
@@ -224,6 +230,10 @@ int pick_cw(int ck, int W) {
         const int cw = std::atoi(s);
         if (col_fn(ck, cw, COL_GS_MAIN, TGT_F32, PREC_F32) && W % cw == 0) return cw;
     }
+    // narrow plans (a single small image) take 2-column tiles: twice the
+    // workgroups per CU, the partner tile reads the other half of each line
+    // through the same XCD's L2 (measured 13.0 -> 10.7 us per 1024^2 pass)
+    if (kPlans[ck].variant == 1 && W % 2 == 0 && col_fn(ck, 2, COL_GS_MAIN, TGT_F32, PREC_F32)) return 2;
     // first tile (in this order) whose complex64 LDS leaves room for two
     // workgroups per CU; 2-column tiles only with >= 8 waves (long columns)
     for (int cw : {4, 8, 16, 2}) {
@@ -241,15 +251,43 @@ int pick_cw(int ck, int W) {
 // when the wide one would leave fewer than 4 waves per SIMD on the chip
 // (e.g. a single 1024^2 hologram), else the wide one. $SLM_PLAN=wide|narrow
 // forces a variant where it exists.
-int pick_plan(int n, long long elems) {
+// Float32 transforms take the narrow plan where the wide one holds more than
+// 16 elements per thread (4096: 32): those are not persistent (kernels.hpp,
+// tile_persistent) and spill.
+int pick_plan(int n, long long elems, int prec) {
     const int wide = plan_index(n, 0), narrow = plan_index(n, 1);
     if (narrow < 0) return wide;
     if (const char* s = std::getenv("SLM_PLAN")) {
         if (!std::strcmp(s, "wide")) return wide;
         if (!std::strcmp(s, "narrow")) return narrow;
     }
+    if (prec == PREC_F32 && kPlans[wide].e > 16 && kPlans[narrow].e <= 16) return narrow;
     const long long waves = elems / kPlans[wide].e / 64;
     return waves < 4LL * 1024 ? narrow : wide;
+}
+
+// Radix plans, tiles and twiddle tables of a plan for one arithmetic precision
+// (slm_plan_create, slm_plan_set_precision).
+int configure(slm_plan* p, int prec) {
+    const long long elems = (long long)p->B * p->holo;
+    const int row_key = pick_plan(p->W, elems, prec);
+    const int col_key = pick_plan(p->H, elems, prec);
+    const int cw = pick_cw(col_key, p->W);
+    if (!cw) return fail(SLM_ERR_UNSUPPORTED, "no column tiling for %dx%d", p->H, p->W);
+    const void *tr = nullptr, *tc = nullptr;
+    RC(get_twiddles(row_key, prec, &tr));
+    RC(get_twiddles(col_key, prec, &tc));
+    p->prec = prec;
+    p->row_key = row_key;
+    p->col_key = col_key;
+    p->cw = cw;
+    p->nwg = p->W / cw;
+    p->col_threads = col_threads(col_key, cw);
+    p->row_threads = row_threads(row_key);
+    p->rpw = row_rpw(row_key);
+    p->tw_row = tr;
+    p->tw_col = tc;
+    return 0;
 }
 
 // Every kernel of a run is launched through here. In a timed run
@@ -312,17 +350,59 @@ ColParams col_params(slm_plan* p) {
     return c;
 }
 
+
+// Grid of a persistent tile loop (kernels.hpp, tile_loop): as many workgroups
+// as the chip holds at once (occupancy query, cached per kernel), never more
+// than there are tiles. $SLM_PERSIST=0 launches one workgroup per tile.
+int tile_grid(const void* fn, int threads, long long tiles, bool persistent, int* grid) {
+    static std::map<const void*, int> resident;
+    static int cus = 0, persist = -1;
+    if (persist < 0) {
+        const char* s = std::getenv("SLM_PERSIST");
+        persist = s ? std::atoi(s) : 1;
+    }
+    if (tiles > INT_MAX) return fail(SLM_ERR_ARG, "%lld tiles exceed one launch", tiles);
+    if (!persist || !persistent) {
+        *grid = (int)tiles;
+        return 0;
+    }
+    if (!cus) {
+        int dev = 0;
+        HIP_TRY(hipGetDevice(&dev));
+        HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    auto it = resident.find(fn);
+    if (it == resident.end()) {
+        int per_cu = 0;
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, 0));
+        it = resident.emplace(fn, std::max(1, per_cu)).first;
+    }
+    *grid = (int)std::min<long long>(tiles, (long long)it->second * cus * persist);
+    return 0;
+}
+
 int launch_row(slm_plan* p, int mode, const RowParams& rp, int cls) {
     RowFn fn = row_fn(p->row_key, mode, p->prec);
     if (!fn) return fail(SLM_ERR_UNSUPPORTED, "no row kernel for width %d mode %d", p->W, mode);
-    return launch(p, cls, fn, dim3(p->H / p->rpw, p->B), dim3(p->row_threads), rp);
+    RowParams r = rp;
+    r.B = p->B;
+    r.ntile = p->H / p->rpw;
+    int grid = 0;
+    RC(tile_grid((const void*)fn, p->row_threads, (long long)r.ntile * p->B,
+                  tile_persistent(p->prec, kPlans[p->row_key].e), &grid));
+    return launch(p, cls, fn, dim3(grid), dim3(p->row_threads), r);
 }
 
 int launch_col(slm_plan* p, int mode, const ColParams& cp, int cls) {
     const int tt = (mode == COL_EXPECTED || mode == COL_FFT_FWD || mode == COL_FFT_INV) ? TGT_F32 : p->tt;
     ColFn fn = col_fn(p->col_key, p->cw, mode, tt, p->prec);
     if (!fn) return fail(SLM_ERR_UNSUPPORTED, "no column kernel for height %d cw %d mode %d", p->H, p->cw, mode);
-    return launch(p, cls, fn, dim3(p->nwg, p->B), dim3(p->col_threads), cp);
+    ColParams c = cp;
+    c.B = p->B;
+    int grid = 0;
+    RC(tile_grid((const void*)fn, p->col_threads, (long long)p->nwg * p->B,
+                  tile_persistent(p->prec, kPlans[p->col_key].e), &grid));
+    return launch(p, cls, fn, dim3(grid), dim3(p->col_threads), c);
 }
 
 StatsParams stats_params(slm_plan* p, double tol) {
@@ -345,11 +425,6 @@ int launch_finalize(slm_plan* p, double tol, int iter) {
     return launch(p, SLM_KERNEL_OTHER, stats_finalize_kernel, dim3(p->B), dim3(256), s);
 }
 
-#define RC(x)                 \
-    do {                      \
-        int rc_ = (x);        \
-        if (rc_) return rc_;  \
-    } while (0)
 
 int enqueue_gs(slm_plan* p, int loops, double tol, int checked) {
     RowParams rp = row_params(p);
@@ -523,22 +598,20 @@ int slm_plan_create(int algo, int batch, int height, int width, int tgt_type, in
     p->max_loops = max_loops;
     p->device = g_device;
     p->holo = (long long)height * width;
-    p->row_key = pick_plan(width, (long long)batch * p->holo);
-    p->col_key = pick_plan(height, (long long)batch * p->holo);
-    p->cw = pick_cw(p->col_key, width);
-    if (!p->cw) {
-        delete p;
-        return fail(SLM_ERR_UNSUPPORTED, "no column tiling for %dx%d", height, width);
-    }
-    p->nwg = width / p->cw;
-    p->col_threads = col_threads(p->col_key, p->cw);
-    p->row_threads = row_threads(p->row_key);
-    p->rpw = row_rpw(p->row_key);
     if (const char* e = std::getenv("SLM_WT")) p->wt = std::atoi(e) != 0;
-    if (const char* e = std::getenv("SLM_PRECISION")) p->prec = (std::strcmp(e, "f32") == 0) ? PREC_F32 : PREC_F64;
-    int rc = get_twiddles(p->row_key, p->prec, &p->tw_row);
-    if (!rc) rc = get_twiddles(p->col_key, p->prec, &p->tw_col);
-    if (rc) {
+    if (const char* e = std::getenv("SLM_PRECISION")) p->prec = (std::strcmp(e, "f64") == 0) ? PREC_F64 : PREC_F32;
+    // buffers indexed by column panel / row group hold the finer tiling of both precisions
+    int max_nwg = 0, min_rpw = INT_MAX;
+    for (int prec : {PREC_F32, PREC_F64}) {
+        int rc = configure(p, prec);
+        if (rc) {
+            delete p;
+            return rc;
+        }
+        max_nwg = std::max(max_nwg, p->nwg);
+        min_rpw = std::min(min_rpw, p->rpw);
+    }
+    if (int rc = configure(p, p->prec)) {
         delete p;
         return rc;
     }
@@ -568,7 +641,7 @@ int slm_plan_create(int algo, int batch, int height, int width, int tgt_type, in
     if (has_ain) RC(alloc((void**)&p->ain, (size_t)p->holo * sizeof(float)));
     RC(alloc((void**)&p->phase_out, n * sizeof(float)));
     RC(alloc((void**)&p->e_out, n * sizeof(float)));
-    RC(alloc((void**)&p->partials, (size_t)batch * max_loops * p->nwg * 4 * sizeof(double)));
+    RC(alloc((void**)&p->partials, (size_t)batch * max_loops * max_nwg * 4 * sizeof(double)));
     RC(alloc((void**)&p->stats, (size_t)batch * max_loops * 4 * sizeof(double)));
     RC(alloc((void**)&p->stop, (size_t)batch * sizeof(int)));
     RC(alloc((void**)&p->norm, (size_t)batch * sizeof(double)));
@@ -576,8 +649,8 @@ int slm_plan_create(int algo, int batch, int height, int width, int tgt_type, in
     RC(alloc((void**)&p->sum_t2, (size_t)batch * sizeof(double)));
     RC(alloc((void**)&p->ts_part, (size_t)batch * kTsBlocks * 2 * sizeof(double)));
     if (const char* e = std::getenv("SLM_TRACE_BUF"); e && std::atoi(e)) {
-        RC(alloc((void**)&p->trace_col, (size_t)batch * p->nwg * 4 * sizeof(unsigned long long)));
-        RC(alloc((void**)&p->trace_row, (size_t)batch * (height / p->rpw) * 4 * sizeof(unsigned long long)));
+        RC(alloc((void**)&p->trace_col, (size_t)batch * max_nwg * 4 * sizeof(unsigned long long)));
+        RC(alloc((void**)&p->trace_row, (size_t)batch * (height / min_rpw) * 4 * sizeof(unsigned long long)));
     }
     *out = p;
     return 0;
@@ -628,12 +701,7 @@ int slm_plan_set_precision(slm_plan* p, int precision) {
     if (precision != SLM_PRECISION_F32 && precision != SLM_PRECISION_F64)
         return fail(SLM_ERR_ARG, "unknown precision %d", precision);
     HIP_TRY(hipSetDevice(p->device));
-    const void *tr = nullptr, *tc = nullptr;
-    RC(get_twiddles(p->row_key, precision, &tr));
-    RC(get_twiddles(p->col_key, precision, &tc));
-    p->prec = precision;
-    p->tw_row = tr;
-    p->tw_col = tc;
+    RC(configure(p, precision));
     return 0;
 }
 

@@ -27,10 +27,16 @@ def summary(tr):
 def main():
     _lib.init(0)
     for cfg in sys.argv[1].split(","):
+        prec = None
+        if cfg.endswith(("f32", "f64")):
+            prec = _lib.PRECISION_F32 if cfg.endswith("f32") else _lib.PRECISION_F64
+            cfg = cfg[:-3]
         n, b = (int(v) for v in cfg.split("x"))
         t = np.random.default_rng(1).uniform(0, 255, (b, n, n)).astype(np.float32)
         with _lib.Plan(_lib.ALGO_GS, b, n, n, _lib.TGT_F32, False, 20) as p:
             p.set_target(t)
+            if prec is not None:
+                p.set_precision(prec)
             p.run(20)
             p.sync()
             for cls in (_lib.KERNEL_COL_MAIN, _lib.KERNEL_ROW_MAIN):
