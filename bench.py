@@ -262,12 +262,12 @@ def main():
         extra = {"pcie_inclusive": pcie_inclusive(plan, targets(0, bper, n), iters)}
         try:
             extra["gs_4096"] = secondary(4096, 1, 20)
-            extra["gs_1024_batch64"] = secondary(1024, 64, 20)
+            extra["gs_4096_batch8"] = secondary(4096, 8, 20)  # configs[4] per GPU at 8 GPUs
+            extra["gs_1024_batch64"] = secondary(1024, 64, 20)  # configs[3] per GPU at 8 GPUs
             extra["gd_1024"] = secondary(1024, 1, 500, algo=_lib.ALGO_GD, reps=2)  # configs[2]
-            f32 = _lib.PRECISION_F32  # float32 butterflies (parity 2.4e-6..5.3e-6 at the 8c gates)
-            extra["f32_gs_1024"] = secondary(1024, 1, 200, precision=f32)
-            extra["f32_gs_4096"] = secondary(4096, 1, 20, precision=f32)
-            extra["f32_gs_1024_batch64"] = secondary(1024, 64, 20, precision=f32)
+            f64 = _lib.PRECISION_F64  # float64 butterflies (parity margin)
+            extra["f64_gs_1024"] = secondary(1024, 1, 200, precision=f64)
+            extra["f64_gs_4096"] = secondary(4096, 1, 20, precision=f64)
         except _lib.SlmError as e:  # pragma: no cover - report, do not hide
             extra["error"] = str(e)
         out["extra"] = extra

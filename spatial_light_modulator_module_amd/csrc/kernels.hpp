@@ -288,7 +288,7 @@ using XchgOf = std::conditional_t<((SLM_F64_XCHG || (kPlans[K].variant == 1 && k
 #ifndef SLM_F64_TWCACHE_MAX
 #define SLM_F64_TWCACHE_MAX 0  // measured neutral at 1024^2 (80 caches the narrow plans)
 #endif
-template <int P, int THREADS, int K>
+template <int P, int THREADS, int K, bool COL>
 constexpr int tw_mode() {
     if constexpr (P == 1)
         return TwCountOf<K, RadicesOf<K>>::value * 4 <= SLM_F64_TWCACHE_MAX && THREADS <= 512 ? TW_CACHED
@@ -296,6 +296,17 @@ constexpr int tw_mode() {
 #ifdef SLM_F32_TW
     return SLM_F32_TW;
 #else
+    // float32 (measured per launch):
+    //  * column kernels of 2048+ lines read the table where used (4096:
+    //    156 -> 127 us, 2048: 109 -> 93 us; registers 208 -> 122, two
+    //    workgroups per CU);
+    //  * everything else caches every twiddle of the thread. (Row kernels that
+    //    form w^2.. from w^1 ran 7-10 % faster at 2048/4096 but took the 4096^2
+    //    warm-start parity from 3.1e-6 to 1.3e-5 rms after 100 iterations.)
+    if constexpr (COL && PlanOf<K>::N >= 2048) return TW_DIRECT;
+#ifdef SLM_F32_ROW_TW
+    if constexpr (!COL) return SLM_F32_ROW_TW;
+#endif
     return THREADS <= 512 && PlanOf<K>::E <= 16 ? TW_CACHED : TW_DIRECT;
 #endif
 }
@@ -425,7 +436,7 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
     const int lrow = qq * QR + q4;
     const long long bstep = (long long)T * p.H;  // slot m adds m * bstep (blocked layout)
     const LdsLine<X> lds{smem + lrow * LINE};
-    Twiddles<K, C, tw_mode<P, RowCfg<K>::THREADS, K>()> tw;
+    Twiddles<K, C, tw_mode<P, RowCfg<K>::THREADS, K, false>()> tw;
     load_twiddles<K, C>(tw, t, p.tw);
 
     // tile = (hologram b, row group g); rows g * RPW + lrow
@@ -552,7 +563,7 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
     const int t = threadIdx.x / CW;
     constexpr long long kStep = 4LL * T;  // blocked layout: row y = t + T m
     const LdsTile<CW, X> lds{smem, c};
-    Twiddles<K, C, tw_mode<P, THREADS, K>()> tw;
+    Twiddles<K, C, tw_mode<P, THREADS, K, true>()> tw;
     load_twiddles<K, C>(tw, t, p.tw);
     constexpr bool kTarget = (MODE == COL_GS_MAIN || MODE == COL_GD_STATS || MODE == COL_GD_GRAD);
     constexpr int NT = kTarget ? E : 1;

@@ -602,6 +602,7 @@ int slm_plan_create(int algo, int batch, int height, int width, int tgt_type, in
     if (const char* e = std::getenv("SLM_PRECISION")) p->prec = (std::strcmp(e, "f64") == 0) ? PREC_F64 : PREC_F32;
     // buffers indexed by column panel / row group hold the finer tiling of both precisions
     int max_nwg = 0, min_rpw = INT_MAX;
+    const int want = p->prec;
     for (int prec : {PREC_F32, PREC_F64}) {
         int rc = configure(p, prec);
         if (rc) {
@@ -611,7 +612,7 @@ int slm_plan_create(int algo, int batch, int height, int width, int tgt_type, in
         max_nwg = std::max(max_nwg, p->nwg);
         min_rpw = std::min(min_rpw, p->rpw);
     }
-    if (int rc = configure(p, p->prec)) {
+    if (int rc = configure(p, want)) {
         delete p;
         return rc;
     }

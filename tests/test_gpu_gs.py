@@ -89,16 +89,20 @@ def test_gs_matches_faithful_oracle(gpu, shape, dtype):
 
 @pytest.mark.gpu
 def test_gs_4096_property(gpu):
-    """4096^2: a few warm iterations against the complex64 model, plus the
-    energy identity sum|C|^2 = S * sum|B|^2 (Parseval) on the expected output."""
+    """4096^2: a few iterations from a random phase against the float64
+    restatement (bar 1e-5; the complex64 NumPy model itself sits ~2e-6 away from
+    float32 butterflies here), plus the energy identity sum|C|^2 = S * sum|B|^2
+    (Parseval) on the expected output."""
     from spatial_light_modulator_module_amd import algorithms as alg
 
     rng = np.random.default_rng(4096)
     t = rng.uniform(0, 255, (4096, 4096)).astype(np.float32)
     phi0 = rng.uniform(-np.pi, np.pi, t.shape).astype(np.float32)
     phase, e, errs, norm, emax = alg.run_gs(t[None], 3, initial_phase=phi0[None])
-    ph_o, e_o, _ = orc.gerchberg_saxton_c64(t, 3, initial_phase=phi0)
-    assert orc.phase_rms(phase[0], ph_o) < 2e-6
+    ph_o, e_o, _ = orc.gerchberg_saxton_faithful(t, 3, initial_phase=phi0)
+    rms = orc.phase_rms(phase[0], ph_o)
+    print(f"[parity] GS 4096^2 random phase x3 vs float64: phase rms {rms:.3e}")
+    assert rms < PHASE_RMS_TOL
     s = t.size
     np.testing.assert_allclose(np.sum(e[0].astype(np.float64)), s * s, rtol=1e-4)  # |B| = 1
 
