@@ -184,7 +184,13 @@ struct slm_plan {
     long long holo = 0;
     hipStream_t stream = nullptr;
     int prec = PREC_F32;  // butterflies/twiddles; parity at both precisions: tests/test_gpu_precision.py
-    int wt = 1;  // write-through field stores ($SLM_WT=0 disables)
+    // write-through field stores per pass ($SLM_WT=0/1 forces both). Measured
+    // (float32): write-through is faster for single images up to 1024^2 (no
+    // dirty L2 at the kernel boundary); columns of 2048+ (2-column tiles:
+    // half lines, merged in L2 before write-back) and rows of launches with
+    // 32M+ elements are faster written back (4096^2 column pass 129 -> 105 us,
+    // 4 x 4096^2 row pass 548 -> 480 us).
+    int wt_col = 1, wt_row = 1;
     unsigned long long* trace_col = nullptr;  // SLM_TRACE diagnostics ($SLM_TRACE_BUF=1)
     unsigned long long* trace_row = nullptr;
     const void* tw_row = nullptr;
@@ -328,7 +334,7 @@ RowParams row_params(slm_plan* p) {
     r.holo = p->holo;
     r.inv_s = (float)(1.0 / (double)p->holo);
     r.tw = p->tw_row;
-    r.wt = p->wt;
+    r.wt = p->wt_row;
     r.trace = p->trace_row;
     return r;
 }
@@ -345,7 +351,7 @@ ColParams col_params(slm_plan* p) {
     c.nwg = p->nwg;
     c.holo = p->holo;
     c.tw = p->tw_col;
-    c.wt = p->wt;
+    c.wt = p->wt_col;
     c.trace = p->trace_col;
     return c;
 }
@@ -598,7 +604,9 @@ int slm_plan_create(int algo, int batch, int height, int width, int tgt_type, in
     p->max_loops = max_loops;
     p->device = g_device;
     p->holo = (long long)height * width;
-    if (const char* e = std::getenv("SLM_WT")) p->wt = std::atoi(e) != 0;
+    p->wt_col = height >= 2048 ? 0 : 1;
+    p->wt_row = (long long)batch * p->holo >= (32LL << 20) ? 0 : 1;
+    if (const char* e = std::getenv("SLM_WT")) p->wt_col = p->wt_row = std::atoi(e) != 0;
     if (const char* e = std::getenv("SLM_PRECISION")) p->prec = (std::strcmp(e, "f64") == 0) ? PREC_F64 : PREC_F32;
     // buffers indexed by column panel / row group hold the finer tiling of both precisions
     int max_nwg = 0, min_rpw = INT_MAX;
