@@ -122,6 +122,23 @@ def test_gs_batch_equals_single(gpu):
 
 
 @pytest.mark.gpu
+def test_gs_4096_batch_equals_single(gpu):
+    """2 x 4096^2 (a 32M-element launch: write-back row stores, DESIGN.md
+    section 3) gives the same bits as each hologram alone (write-through rows)."""
+    from spatial_light_modulator_module_amd import algorithms as alg
+
+    rng = np.random.default_rng(8192)
+    t = rng.uniform(0, 255, (2, 4096, 4096)).astype(np.float32)
+    phi0 = rng.uniform(-np.pi, np.pi, t.shape).astype(np.float32)
+    pb, _, errb, _, _ = alg.run_gs(t, 3, initial_phase=phi0)
+    for k in range(2):
+        p1, _, err1, _, _ = alg.run_gs(t[k:k + 1], 3, initial_phase=phi0[k:k + 1])
+        np.testing.assert_array_equal(pb[k], p1[0])
+        assert errb[k] == err1[0]
+    alg.clear_plans()
+
+
+@pytest.mark.gpu
 def test_gs_tolerance_stop_vs_reference(gpu, golden_dir):
     from spatial_light_modulator_module_amd import algorithms as alg
 
