@@ -127,10 +127,14 @@ struct RowCfg {
     // pairs: twice the workgroups, measured 11.6 -> 9.1 us per 1024^2 row pass.
     static constexpr bool kPairs = (4 * PlanOf<K>::ROWSTRIDE * 8 > kLdsPair && (SLM_ROW_PAIRS || T >= 256)) ||
                                    kPlans[K].variant == 1;
+    // 4096 narrow rows (256 threads per row) run one row per workgroup: two
+    // workgroups of 4 waves per CU instead of one of 8 (8 x 4096^2 row pass
+    // 931 -> 755 us with write-back stores)
+    static constexpr bool kSingle = kPlans[K].variant == 1 && PlanOf<K>::N >= 4096;
 #ifdef SLM_ROW_RPW
     static constexpr int RPW = (T >= 64) ? SLM_ROW_RPW : 256 / T;
 #else
-    static constexpr int RPW = (T >= 64) ? (kPairs ? 2 : 4) : 256 / T;
+    static constexpr int RPW = (T >= 64) ? (kSingle ? 1 : kPairs ? 2 : 4) : 256 / T;
 #endif
     static constexpr int QR = RPW < 4 ? RPW : 4;  // rows interleaved across a wave
     static constexpr int THREADS = RPW * T;

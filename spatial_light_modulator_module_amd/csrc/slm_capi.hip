@@ -187,9 +187,9 @@ struct slm_plan {
     // write-through field stores per pass ($SLM_WT=0/1 forces both). Measured
     // (float32): write-through is faster for single images up to 1024^2 (no
     // dirty L2 at the kernel boundary); columns of 2048+ (2-column tiles:
-    // half lines, merged in L2 before write-back) and rows of launches with
-    // 32M+ elements are faster written back (4096^2 column pass 129 -> 105 us,
-    // 4 x 4096^2 row pass 548 -> 480 us).
+    // half lines, merged in L2 before write-back) and rows of 4096 or of
+    // launches with 32M+ elements are faster written back (4096^2 column pass
+    // 129 -> 105 us, 4 x 4096^2 row pass 548 -> 480 us).
     int wt_col = 1, wt_row = 1;
     unsigned long long* trace_col = nullptr;  // SLM_TRACE diagnostics ($SLM_TRACE_BUF=1)
     unsigned long long* trace_row = nullptr;
@@ -605,7 +605,7 @@ int slm_plan_create(int algo, int batch, int height, int width, int tgt_type, in
     p->device = g_device;
     p->holo = (long long)height * width;
     p->wt_col = height >= 2048 ? 0 : 1;
-    p->wt_row = (long long)batch * p->holo >= (32LL << 20) ? 0 : 1;
+    p->wt_row = ((long long)batch * p->holo >= (32LL << 20) || width >= 4096) ? 0 : 1;
     if (const char* e = std::getenv("SLM_WT")) p->wt_col = p->wt_row = std::atoi(e) != 0;
     if (const char* e = std::getenv("SLM_PRECISION")) p->prec = (std::strcmp(e, "f64") == 0) ? PREC_F64 : PREC_F32;
     // buffers indexed by column panel / row group hold the finer tiling of both precisions
