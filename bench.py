@@ -182,7 +182,11 @@ def secondary(n, batch, iters, algo=_lib.ALGO_GS, precision=None, reps=3):
         dom, rows, _, _ = kernel_roofline(plan, iters, wa)
         info = plan.info()
     iter_ms = wall / iters * 1e3
-    return {"algo": "gd" if algo == _lib.ALGO_GD else "gs", "shape": [batch, n, n], "iters": iters,
+    name = "gd" if algo == _lib.ALGO_GD else "gs"
+    traffic = pmc_traffic(f"{name}_{n}x{n}_b{batch}_it{iters}_{info['precision']}")  # rocprofv3 PMC, profiles/
+    for k, row in rows.items():
+        row["traffic_bytes_per_launch"] = None if traffic is None else traffic.get(k)
+    return {"algo": name, "shape": [batch, n, n], "iters": iters,
             "holograms_per_s": batch / wall, "iter_ms": iter_ms, "iter_ms_per_hologram": iter_ms / batch,
             "kernels": rows, "dominant": dom,
             "dominant_frac_of_hbm_peak": round(rows[dom]["achieved_gbs"] / HBM_PEAK_GBS, 4), "tiling": info}
