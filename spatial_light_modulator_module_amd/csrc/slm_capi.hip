@@ -217,6 +217,14 @@ struct slm_plan {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
     std::vector<int> ev_class;
     size_t ev_used = 0;
+    // replayed run (default; SLM_GRAPH=0 launches kernel by kernel): the whole
+    // enqueue_run captured once per (loops, tol, checked, wa, warm-start state)
+    // and relaunched as one graph -- 3 % per 1024^2 GS iteration, 6 % at 256^2
+    // (gpurun_out/exp17: the inter-kernel gaps of 400 dependent launches)
+    hipGraphExec_t gexec = nullptr;
+    int g_loops = -1, g_checked = -1, g_state = -1;
+    double g_tol = 0.0;
+    float g_wa = 0.f;
 };
 
 namespace {
@@ -542,6 +550,7 @@ void free_plan(slm_plan* p) {
         (void)hipEventDestroy(e.first);
         (void)hipEventDestroy(e.second);
     }
+    if (p->gexec) (void)hipGraphExecDestroy(p->gexec);
     if (p->stream) (void)hipStreamDestroy(p->stream);
     delete p;
 }
@@ -772,7 +781,39 @@ int slm_plan_set_lr(slm_plan* p, const float* lr) {
 
 int slm_plan_run(slm_plan* p, int loops, double tol, int checked, float wa) {
     if (p) p->timing = false;
-    return enqueue_run(p, loops, tol, checked, wa);
+    static const bool use_graph = [] {
+        const char* e = std::getenv("SLM_GRAPH");
+        return !e || std::atoi(e) != 0;
+    }();
+    if (!p || !use_graph) return enqueue_run(p, loops, tol, checked, wa);
+    const int state = (p->phase_set ? 1 : 0) | (p->field_set ? 2 : 0);
+    if (!p->gexec || p->g_state != state || p->g_loops != loops || p->g_tol != tol || p->g_checked != checked || p->g_wa != wa) {
+        if (p->gexec) {
+            HIP_TRY(hipGraphExecDestroy(p->gexec));
+            p->gexec = nullptr;
+        }
+        HIP_TRY(hipSetDevice(p->device));
+        HIP_TRY(hipStreamBeginCapture(p->stream, hipStreamCaptureModeThreadLocal));
+        int rc = enqueue_run(p, loops, tol, checked, wa);
+        hipGraph_t g = nullptr;
+        hipError_t e = hipStreamEndCapture(p->stream, &g);
+        if (rc) {
+            if (g) (void)hipGraphDestroy(g);
+            return rc;
+        }
+        HIP_TRY(e);
+        e = hipGraphInstantiate(&p->gexec, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        HIP_TRY(e);
+        p->g_loops = loops;
+        p->g_tol = tol;
+        p->g_checked = checked;
+        p->g_wa = wa;
+        p->g_state = state;
+    }
+    HIP_TRY(hipSetDevice(p->device));
+    HIP_TRY(hipGraphLaunch(p->gexec, p->stream));
+    return 0;
 }
 
 int slm_plan_run_timed(slm_plan* p, int loops, double tol, int checked, float wa, double* us, int* counts) {
