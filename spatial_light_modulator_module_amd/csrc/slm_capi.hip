@@ -291,6 +291,10 @@ int configure(slm_plan* p, int prec) {
     const void *tr = nullptr, *tc = nullptr;
     RC(get_twiddles(row_key, prec, &tr));
     RC(get_twiddles(col_key, prec, &tc));
+    if (p->gexec) {  // the captured run bakes in kernels and tables
+        HIP_TRY(hipGraphExecDestroy(p->gexec));
+        p->gexec = nullptr;
+    }
     p->prec = prec;
     p->row_key = row_key;
     p->col_key = col_key;
