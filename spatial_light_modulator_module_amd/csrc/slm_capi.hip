@@ -268,14 +268,22 @@ int pick_cw(int ck, int W) {
 // Float32 transforms take the narrow plan where the wide one holds more than
 // 16 elements per thread (4096: 32): those are not persistent (kernels.hpp,
 // tile_persistent) and spill.
-int pick_plan(int n, long long elems, int prec) {
+int pick_plan(int n, long long elems, int prec, bool row = false) {
     const int wide = plan_index(n, 0), narrow = plan_index(n, 1);
     if (narrow < 0) return wide;
+    if (const char* s = std::getenv(row ? "SLM_ROW_PLAN" : "SLM_COL_PLAN")) {
+        if (!std::strcmp(s, "wide")) return wide;
+        if (!std::strcmp(s, "narrow")) return narrow;
+    }
     if (const char* s = std::getenv("SLM_PLAN")) {
         if (!std::strcmp(s, "wide")) return wide;
         if (!std::strcmp(s, "narrow")) return narrow;
     }
     if (prec == PREC_F32 && kPlans[wide].e > 16 && kPlans[narrow].e <= 16) return narrow;
+    // 2048-point rows: the 4-pass E = 8 plan beats the 3-pass E = 16 one at
+    // every batch (gpurun_out/exp19: 1 image 26.7 -> 21.7 us, 16 images
+    // 405 -> 292 us per row launch); columns keep the rule below
+    if (row && prec == PREC_F32 && n == 2048) return narrow;
     const long long waves = elems / kPlans[wide].e / 64;
     return waves < 4LL * 1024 ? narrow : wide;
 }
@@ -284,7 +292,7 @@ int pick_plan(int n, long long elems, int prec) {
 // (slm_plan_create, slm_plan_set_precision).
 int configure(slm_plan* p, int prec) {
     const long long elems = (long long)p->B * p->holo;
-    const int row_key = pick_plan(p->W, elems, prec);
+    const int row_key = pick_plan(p->W, elems, prec, true);
     const int col_key = pick_plan(p->H, elems, prec);
     const int cw = pick_cw(col_key, p->W);
     if (!cw) return fail(SLM_ERR_UNSUPPORTED, "no column tiling for %dx%d", p->H, p->W);
