@@ -300,6 +300,7 @@ int configure(slm_plan* p, int prec) {
     RC(get_twiddles(row_key, prec, &tr));
     RC(get_twiddles(col_key, prec, &tc));
     if (p->gexec) {  // the captured run bakes in kernels and tables
+        HIP_TRY(hipStreamSynchronize(p->stream));  // a queued replay still owns the exec
         HIP_TRY(hipGraphExecDestroy(p->gexec));
         p->gexec = nullptr;
     }
@@ -800,11 +801,13 @@ int slm_plan_run(slm_plan* p, int loops, double tol, int checked, float wa) {
     if (!p || !use_graph) return enqueue_run(p, loops, tol, checked, wa);
     const int state = (p->phase_set ? 1 : 0) | (p->field_set ? 2 : 0);
     if (!p->gexec || p->g_state != state || p->g_loops != loops || p->g_tol != tol || p->g_checked != checked || p->g_wa != wa) {
+        HIP_TRY(hipSetDevice(p->device));
         if (p->gexec) {
+            // runs are asynchronous: a replay of this exec may still be queued
+            HIP_TRY(hipStreamSynchronize(p->stream));
             HIP_TRY(hipGraphExecDestroy(p->gexec));
             p->gexec = nullptr;
         }
-        HIP_TRY(hipSetDevice(p->device));
         HIP_TRY(hipStreamBeginCapture(p->stream, hipStreamCaptureModeThreadLocal));
         int rc = enqueue_run(p, loops, tol, checked, wa);
         hipGraph_t g = nullptr;

@@ -1,0 +1,165 @@
+"""Parity of every kernel instantiation that bench.py quotes (BASELINE.json configs).
+
+Each test asserts the plan keys / tiles it runs (plan.info()) so a change in
+the plan picker cannot silently move a bench line onto untested kernels:
+
+* configs[3] per GPU: 64 x 1024^2 GS -> wide 1024 plan (key 5), 4-column tiles;
+* configs[2]: GD 1024^2, 500 iterations -> narrow 1024 plan (key 11);
+* configs[4] per GPU / north star: 4096^2 GS -> narrow 4096 plan (key 13),
+  gated at 100 warm-start iterations;
+* the column tile widths that give 512- and 1024-thread workgroups (the
+  exchange race fixed in 6e0b072 lived there) against the default tiles.
+
+Oracle: oracle/fast_f64.py (float64, pinned to the reference goldens in
+tests/test_oracle_golden.py), run on the host's CPU share.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import fast_f64
+from oracle import gs_gd_oracle as orc
+
+PHASE_RMS_TOL = 1e-5  # north_star: <= 1e-5 rms on the output phase
+
+
+def bench_targets(first, count, n):
+    """bench.py's synthetic targets: default_rng(1234 + b).uniform(0, 255) float32."""
+    return np.stack([np.random.default_rng(1234 + b).uniform(0, 255, (n, n)).astype(np.float32)
+                     for b in range(first, first + count)])
+
+
+class plan_env:
+    """Temporarily set plan-picker environment overrides (read at plan creation)."""
+
+    def __init__(self, **kw):
+        self.kw = kw
+
+    def __enter__(self):
+        self.old = {k: os.environ.get(k) for k in self.kw}
+        os.environ.update({k: str(v) for k, v in self.kw.items()})
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def gs_run(lib, t, loops, phase=None):
+    b, h, w = t.shape
+    with lib.Plan(lib.ALGO_GS, b, h, w, lib.TGT_F32, False, loops) as p:
+        p.set_target(t)
+        p.set_phase(phase)
+        p.run(loops)
+        ph, e, stats, _ = p.read()
+        return ph, e, stats, p.info()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_gs_1024_batch64_wide_plan(gpu):
+    """configs[3]'s per-GPU slice (64 x 1024^2) on the kernels the bench times:
+    warm-start parity of two holograms vs the float64 oracle, and bitwise
+    equality of holograms 0 and 63 with single-hologram runs of the same plan."""
+    lib = gpu
+    n, b, loops = 1024, 64, 200
+    t = bench_targets(0, b, n)
+    rng = np.random.default_rng(64)
+    phi = rng.uniform(-np.pi, np.pi, (b, n, n)).astype(np.float32)
+    warm = {}
+    for k in (0, 1):
+        phi_k, _, _ = fast_f64.gerchberg_saxton_f64(t[k], 30)
+        phi[k] = phi_k.astype(np.float32)
+        warm[k] = phi[k]
+    ph, e, stats, info = gs_run(lib, t, loops, phi)
+    assert (info["row_plan"], info["col_plan"], info["col_cw"]) == (5, 5, 4), info
+    for k in (0, 1):
+        ref, _, ref_err = fast_f64.gerchberg_saxton_f64(t[k], loops, initial_phase=warm[k])
+        rms = orc.phase_rms(ph[k], ref)
+        print(f"[parity] 64 x 1024^2 wide plan, hologram {k}: warm-start 30+{loops} phase rms {rms:.3e}")
+        assert rms < PHASE_RMS_TOL
+        np.testing.assert_allclose(stats[k, :loops, 3], ref_err, rtol=1e-4)
+    with plan_env(SLM_PLAN="wide"):
+        for k in (0, b - 1):
+            p1, e1, s1, info1 = gs_run(lib, t[k:k + 1], loops, phi[k:k + 1])
+            assert (info1["row_plan"], info1["col_plan"], info1["col_cw"]) == (5, 5, 4)
+            np.testing.assert_array_equal(p1[0], ph[k])
+            np.testing.assert_array_equal(e1[0], e[k])
+            np.testing.assert_array_equal(s1[0], stats[k])
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_gd_1024_configs2(gpu):
+    """configs[2]: GD 1024^2 (lr 0.005, white_attention 1, random guess seed 42):
+    100 iterations at <= 1e-5 rms phase, 500 iterations on the error curve
+    (rtol 1e-3; the float32 phase floor after 500 is ~5e-5)."""
+    from spatial_light_modulator_module_amd import algorithms as alg
+
+    lib = gpu
+    n = 1024
+    t = bench_targets(0, 1, n)[0]
+    x0 = alg.make_initial_guess("random", None, t, 42)
+    res = {}
+    for loops in (100, 500):
+        with lib.Plan(lib.ALGO_GD, 1, n, n, lib.TGT_F32, False, loops) as p:
+            info = p.info()
+            assert (info["row_plan"], info["col_plan"], info["col_cw"]) == (11, 11, 2), info
+            p.set_target(t[None])
+            p.set_field(x0[None])
+            p.set_lr(np.full(loops, 0.005, np.float32))
+            p.run(loops, white_attention=1.0)
+            ph, _, stats, _ = p.read(expected=False)
+            res[loops] = (ph[0], stats[0, :loops, 3])
+    ph100, _, err100, x100 = fast_f64.gradient_descent_f64(t, 100, 0.005, 1.0, initial_field=x0)
+    rms = orc.phase_rms(res[100][0], ph100)
+    print(f"[parity] GD 1024^2 100 iterations: phase rms {rms:.3e}")
+    assert rms < PHASE_RMS_TOL
+    np.testing.assert_allclose(res[100][1], err100, rtol=1e-4)
+    ph500, _, err400, _ = fast_f64.gradient_descent_f64(t, 400, 0.005, 1.0, initial_field=x100)
+    np.testing.assert_allclose(res[500][1], np.concatenate([err100, err400]), rtol=1e-3)
+    rms = orc.phase_rms(res[500][0], ph500)
+    print(f"[parity] GD 1024^2 500 iterations: phase rms {rms:.3e} (float32 floor ~5e-5)")
+    assert rms < 2e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_gs_4096_warm_start_gate(gpu):
+    """North-star shape: 4096^2 GS warm-started from a 30-iteration state, then
+    100 iterations vs the float64 oracle at <= 1e-5 rms (the 100-iteration gate
+    of SURVEY.md 8c; 200 iterations drift to the bar in complex64 state)."""
+    lib = gpu
+    n, span = 4096, 100
+    t = bench_targets(0, 1, n)
+    _, _, _, info = gs_run(lib, t, 1)
+    assert (info["row_plan"], info["col_plan"], info["col_cw"]) == (13, 13, 2), info
+    ph30, _, _, _ = gs_run(lib, t, 30)  # any warmed state serves (the GS state is angle(A) only)
+    ph, _, stats, _ = gs_run(lib, t, span, ph30)
+    ref, _, ref_err = fast_f64.gerchberg_saxton_f64(t[0], span, initial_phase=ph30[0])
+    rms = orc.phase_rms(ph[0], ref)
+    print(f"[parity] 4096^2 warm-start 30+{span}: phase rms {rms:.3e}")
+    assert rms < PHASE_RMS_TOL
+    np.testing.assert_allclose(stats[0, :span, 3], ref_err, rtol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cw", [8, 16])
+def test_column_tile_widths_bitwise(gpu, cw):
+    """512- and 1024-thread column workgroups (cw x 64 threads on the wide 1024
+    plan) give the bits of the default 4-column tiles, run after run: the LDS
+    exchange race of 6e0b072 showed up as ~1.5 % of launches differing here."""
+    lib = gpu
+    t = bench_targets(0, 4, 1024)
+    phi = np.random.default_rng(cw).uniform(-np.pi, np.pi, t.shape).astype(np.float32)
+    ref = gs_run(lib, t, 40, phi)
+    assert ref[3]["col_cw"] == 4 and ref[3]["col_plan"] == 5
+    with plan_env(SLM_COL_CW=cw):
+        for _ in range(3):
+            ph, e, stats, info = gs_run(lib, t, 40, phi)
+            assert info["col_cw"] == cw and info["col_threads"] == cw * 64
+            np.testing.assert_array_equal(ph, ref[0])
+            np.testing.assert_array_equal(stats, ref[2])

@@ -23,7 +23,7 @@ import scipy.fft as sfft
 from oracle import gs_gd_oracle as orc
 
 PHASE_RMS_TOL = 1e-5
-WORKERS = min(32, os.cpu_count() or 1)
+WORKERS = min(16, os.cpu_count() or 1)  # the GPU box gives a process a 16-CPU share
 
 
 def _gpu_warm_run(lib, t, phi_w, span, precision):

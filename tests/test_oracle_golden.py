@@ -123,3 +123,70 @@ def test_error_expansion_matches_direct():
     direct = orc.error_f(e * (t.max() / e.max()), t, t.size)
     stats = np.array([e.max(), np.sum(e * e), np.sum(e * t)])
     np.testing.assert_allclose(orc.error_from_stats(stats, t.max(), np.sum(t * t), t.size), direct, rtol=1e-9)
+
+
+# ---------------------------------------------------------------------------
+# the multi-threaded float64 restatements (oracle/fast_f64.py) used by the
+# large-size GPU gates: pinned to the reference goldens and the faithful path
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("name", ["g1_gs_u8_256.npz", "g2_gs_f32_256.npz"])
+def test_fast_gs_warm_start_matches_reference(golden_dir, name):
+    from oracle import fast_f64
+
+    g = load(golden_dir, name)
+    phi, exp, err = fast_f64.gerchberg_saxton_f64(g["target"], 200, initial_phase=g["phi30"], workers=4)
+    # z/|z| in place of exp(1j angle z): rounding-level differences only
+    assert orc.phase_rms(phi, g["phi230"]) < 1e-12
+    np.testing.assert_allclose(err, g["err230"][30:], rtol=1e-11)
+    np.testing.assert_allclose(exp.astype(np.float32), g["expected230"], rtol=1e-5)
+
+
+def test_fast_gs_incoming_intensity_and_tolerance(golden_dir):
+    from PIL import Image
+
+    from oracle import fast_f64
+
+    g = load(golden_dir, "g8_gs_ain_128.npz")
+    # float64 intensity: with the uint8 PNG itself np.sqrt gives float16 and the
+    # reference's whole loop runs in complex64 (the faithful restatement and the
+    # g8 golden cover that dtype flow); the fast oracle is the float64 model
+    img = np.array(Image.open(os.path.join(golden_dir, "g8_incoming_128.png"))).astype(np.float64)
+    phi, _, err = fast_f64.gerchberg_saxton_f64(g["target"], 30, initial_phase=g["phi10"], incoming_intensity=img,
+                                                workers=2)
+    ref_phi, _, ref_err = orc.gerchberg_saxton_faithful(g["target"], 30, incoming_intensity=img,
+                                                        initial_phase=g["phi10"])
+    assert orc.phase_rms(phi, ref_phi) < 1e-12
+    np.testing.assert_allclose(err, ref_err, rtol=1e-11)
+    t3 = load(golden_dir, "g3_gs_traps_128.npz")["target"]
+    _, _, err_tol = fast_f64.gerchberg_saxton_f64(t3, 60, tolerance=1e9, workers=2)
+    assert len(err_tol) == len(load(golden_dir, "g7_edges.npz")["tol_hit_err"])
+
+
+def test_fast_gd_matches_reference(golden_dir):
+    from oracle import fast_f64
+
+    g = load(golden_dir, "g4_gd_f32_256.npz")
+    t = g["target"]
+    x0 = orc.make_initial_guess("random", np.ones(t.shape), t, 42)
+    phi, out, err, x = fast_f64.gradient_descent_f64(t, 100, 0.005, 1.0, initial_field=x0, workers=4)
+    assert orc.phase_rms(phi, g["phi100"]) < 1e-11
+    np.testing.assert_allclose(err, g["err100"], rtol=1e-11)
+    np.testing.assert_allclose(out.astype(np.float32), g["output100"], rtol=1e-5, atol=1e-3)
+    # continuing from the returned field reproduces one long run
+    phi5, _, err5, _ = fast_f64.gradient_descent_f64(t, 400, 0.005, 1.0, initial_field=x, workers=4)
+    np.testing.assert_allclose(np.concatenate([err, err5]), g["err500"], rtol=1e-9)
+    assert orc.phase_rms(phi5, g["phi500"]) < 1e-6  # the golden phi500 is stored as float32
+
+
+def test_fast_gd_unsettle_schedule_matches_faithful():
+    from oracle import fast_f64
+
+    rng = np.random.default_rng(5)
+    t = rng.integers(0, 256, (64, 64)).astype(np.uint8)
+    rates, lr_after = orc.unsettle_schedule(0.003, 30, 2, 30)
+    x0 = orc.make_initial_guess("random", np.ones(t.shape), t, 9)
+    phi, _, err, _ = fast_f64.gradient_descent_f64(t, 30, rates, 1.5, initial_field=x0, workers=1)
+    ref_phi, _, ref_err, ref_lr = orc.gradient_descent_faithful(t, 30, 0.003, 1.5, 2, random_seed=9)
+    assert lr_after == ref_lr
+    assert orc.phase_rms(phi, ref_phi) < 1e-11
+    np.testing.assert_allclose(err, ref_err, rtol=1e-11)
