@@ -9,21 +9,27 @@ by the RCCL gather of the final phase arrays to rank 0. Default workload is
 BASELINE.json configs[1]: a single 1024x1024 float32 random-amplitude target,
 200 iterations, per GPU (weak scaling: N GPUs process N x batch holograms).
 
-For N > 1 the driver launches one process per GPU with torch.distributed.run;
-torch.distributed (gloo, CPU) is only the control plane (barriers, max of the
-per-rank times, broadcast of the RCCL unique id). The data path is
-libslm_hip.so: its kernels and its RCCL send/recv gather over xGMI.
+N > 1: one process per GPU. Under torch.distributed.run (the driver's
+launcher) the ranks come from its environment; `--gpus N` without one makes
+this script its own launcher: it starts N child processes (RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_* set, before any GPU call) and exits with their status.
+No torch in the ranks: the control plane (RCCL unique-id hand-off, barriers,
+the max of per-rank times) is parallel.Group (stdlib TCP), the data path is
+libslm_hip.so -- its kernels and its RCCL send/recv gather over xGMI.
 
 Rank 0 prints ONE JSON line with the metric, a roofline object for the
 dominant kernel (HIP-event timing of every launch of a separately replayed,
-identical run) and the CPU baseline (the repo's NumPy oracle, 1 core, on a
-bounded sample of the same workload, rank 0 at N=1 only).
+identical run; SURVEY.md 8d byte model and the fused kernels' physical bytes,
+both labelled) and the CPU baseline (the repo's NumPy oracle, 1 core and all
+cores of the host share, on a bounded sample of the same workload, rank 0 at
+N=1 only).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -32,8 +38,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# libslm_hip.so (torch is imported ahead of it: one HIP runtime per process)
-from spatial_light_modulator_module_amd import _lib  # noqa: E402
+from spatial_light_modulator_module_amd import _lib, parallel  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
@@ -53,39 +58,16 @@ def parse():
     return ap.parse_args()
 
 
-class Dist:
-    """Control plane: gloo process group when launched with WORLD_SIZE > 1."""
-
-    def __init__(self):
-        self.world = int(os.environ.get("WORLD_SIZE", "1"))
-        self.rank = int(os.environ.get("RANK", "0"))
-        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-        self.pg = None
-        if self.world > 1:
-            import torch.distributed as dist
-
-            dist.init_process_group("gloo")
-            self.dist = dist
-
-    def barrier(self):
-        if self.world > 1:
-            self.dist.barrier()
-
-    def max(self, v: float) -> float:
-        if self.world == 1:
-            return v
-        import torch
-
-        t = torch.tensor([v], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-        return float(t.item())
-
-    def bcast_bytes(self, b: bytes | None) -> bytes:
-        if self.world == 1:
-            return b
-        obj = [b]
-        self.dist.broadcast_object_list(obj, src=0)
-        return obj[0]
+def launch_ranks(n: int) -> int:
+    """bench.py --gpus N outside a launcher: N child processes, one per GPU."""
+    port = parallel.free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SLM_RDZV_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    return max(abs(rc) for rc in rcs)
 
 
 def targets(first: int, count: int, n: int) -> np.ndarray:
@@ -94,19 +76,39 @@ def targets(first: int, count: int, n: int) -> np.ndarray:
                      for b in range(first, first + count)])
 
 
+def model_bytes(plan, cls):
+    """SURVEY.md 8d algorithmic bytes per launch (unfused-pass byte model):
+    GS 68 B/px/iteration = column passes 32 + target 4 (col_main) + row passes
+    32 (row_main); GD 76 = column passes 32 + target 4 (col_main) + row passes
+    16 + gradient epilogue 24 (row_main); the GD statistics pass re-reads X and
+    is not in the model (0). A uint8 target counts 1 B, a_in adds 4 B."""
+    px = plan.batch * plan.height * plan.width
+    tb = 1 if plan.tgt_type == _lib.TGT_U8 else 4
+    ab = 4 if plan.has_ain else 0
+    if cls == _lib.KERNEL_COL_MAIN:
+        return px * (32 + tb)
+    if cls == _lib.KERNEL_ROW_MAIN:
+        return px * (32 + ab + (8 if plan.algo == _lib.ALGO_GD else 0))
+    return 0
+
+
 def kernel_roofline(plan, iters, white_attention=0.0):
     """Time every launch of one run with HIP events on the plan's stream and
-    price the dominant kernel class with its algorithmic bytes."""
+    price each kernel class with both byte models: SURVEY.md 8d's (the
+    roofline numerator, `achieved`) and the bytes the fused kernel physically
+    reads and writes (`physical`, slm_plan_kernel_bytes)."""
     us, cnt = plan.run_timed(iters, white_attention=white_attention)
     rows = {}
     for cls in (_lib.KERNEL_COL_MAIN, _lib.KERNEL_ROW_MAIN, _lib.KERNEL_GD_STATS):
         if cnt[cls] == 0:
             continue
         avg_us = us[cls] / cnt[cls]
-        nbytes = plan.kernel_bytes(cls)
+        phys = plan.kernel_bytes(cls)
+        model = model_bytes(plan, cls)
         rows[_lib.KERNEL_CLASS_NAMES[cls]] = {
-            "avg_us": avg_us, "launches": int(cnt[cls]), "total_us": float(us[cls]), "bytes_per_launch": nbytes,
-            "achieved_gbs": nbytes / (avg_us * 1e-6) / 1e9}
+            "avg_us": avg_us, "launches": int(cnt[cls]), "total_us": float(us[cls]),
+            "model_bytes_per_launch": model, "physical_bytes_per_launch": phys,
+            "achieved_gbs": model / (avg_us * 1e-6) / 1e9, "physical_gbs": phys / (avg_us * 1e-6) / 1e9}
     dom = max(rows, key=lambda k: rows[k]["total_us"])
     return dom, rows, us, cnt
 
@@ -123,8 +125,9 @@ def pmc_traffic(config_key: str):
 
 
 def cpu_baseline(n: int, iters: int, budget_s: float):
-    """The repo's NumPy restatement (faithful float64, scipy.fft single thread,
-    1 core) on the same synthetic target, k iterations, extrapolated."""
+    """The repo's NumPy restatement of the reference (faithful float64, scipy.fft
+    single thread, 1 core, as the reference runs) on the same synthetic target,
+    k iterations, extrapolated to `iters`."""
     from oracle import gs_gd_oracle as orc
 
     t = targets(0, 1, n)[0]
@@ -136,11 +139,33 @@ def cpu_baseline(n: int, iters: int, budget_s: float):
     orc.gerchberg_saxton_faithful(t, k)
     dt = time.perf_counter() - t0
     per_iter = dt / k
-    holo_s = 1.0 / (per_iter * iters)
-    return {"value": holo_s, "unit": "holograms/s", "cores": 1, "kind": "port",
-            "sample": f"{k} GS iterations of the NumPy/SciPy float64 restatement (oracle/gs_gd_oracle.py) on one "
-                      f"{n}x{n} float32 target in {dt:.1f} s, extrapolated to {iters} iterations per hologram",
+    return {"value": 1.0 / (per_iter * iters), "unit": "holograms/s", "cores": 1, "kind": "port",
+            "sample": f"{k} GS iterations of the NumPy/SciPy float64 restatement (oracle/gs_gd_oracle.py, "
+                      f"single-threaded like the reference) on one {n}x{n} float32 target in {dt:.1f} s, "
+                      f"extrapolated to {iters} iterations per hologram",
             "ms_per_iter": per_iter * 1e3, "host_cpus": os.cpu_count()}
+
+
+def cpu_baseline_all_cores(n: int, iters: int, budget_s: float):
+    """The multi-threaded float64 restatement (oracle/fast_f64.py: pocketfft and
+    element-wise work over the host share's threads) on the same target."""
+    from oracle import fast_f64
+
+    workers = fast_f64.DEFAULT_WORKERS
+    t = targets(0, 1, n)[0]
+    phi = np.zeros(t.shape, np.float32)
+    t0 = time.perf_counter()
+    fast_f64.gerchberg_saxton_f64(t, 2, initial_phase=phi, workers=workers)
+    per_iter = (time.perf_counter() - t0) / 2
+    k = int(max(3, min(iters, budget_s / max(per_iter, 1e-6))))
+    t0 = time.perf_counter()
+    fast_f64.gerchberg_saxton_f64(t, k, initial_phase=phi, workers=workers)
+    dt = time.perf_counter() - t0
+    per_iter = dt / k
+    return {"value": 1.0 / (per_iter * iters), "unit": "holograms/s", "cores": workers, "kind": "port",
+            "sample": f"{k} GS iterations of the threaded float64 restatement (oracle/fast_f64.py, {workers} "
+                      f"threads) on one {n}x{n} float32 target in {dt:.1f} s, extrapolated to {iters} iterations",
+            "ms_per_iter": per_iter * 1e3}
 
 
 def pcie_inclusive(plan, host_targets, iters, reps=5):
@@ -156,10 +181,14 @@ def pcie_inclusive(plan, host_targets, iters, reps=5):
             "includes": "target upload + relayout, run, phase download (pageable host memory)"}
 
 
+def _round(v):
+    return round(v, 4) if isinstance(v, float) else v
+
+
 def secondary(n, batch, iters, algo=_lib.ALGO_GS, precision=None, reps=3):
     """Extra single-GPU measurements: one-run wall time and the per-kernel
     roofline of another configuration (4096^2 HBM stress, batched 1024^2, GD,
-    float32 butterflies)."""
+    float64 butterflies)."""
     t = targets(0, batch, n)
     with _lib.Plan(algo, batch, n, n, _lib.TGT_F32, False, iters) as plan:
         plan.set_target(t)
@@ -181,31 +210,39 @@ def secondary(n, batch, iters, algo=_lib.ALGO_GS, precision=None, reps=3):
         wall = (time.perf_counter() - t0) / reps
         dom, rows, _, _ = kernel_roofline(plan, iters, wa)
         info = plan.info()
-    iter_ms = wall / iters * 1e3
+    iter_s = wall / iters
     name = "gd" if algo == _lib.ALGO_GD else "gs"
     traffic = pmc_traffic(f"{name}_{n}x{n}_b{batch}_it{iters}_{info['precision']}")  # rocprofv3 PMC, profiles/
     for k, row in rows.items():
         row["traffic_bytes_per_launch"] = None if traffic is None else traffic.get(k)
+    per_px = 76 if algo == _lib.ALGO_GD else 68
     return {"algo": name, "shape": [batch, n, n], "iters": iters,
-            "holograms_per_s": batch / wall, "iter_ms": iter_ms, "iter_ms_per_hologram": iter_ms / batch,
-            "kernels": rows, "dominant": dom,
-            "dominant_frac_of_hbm_peak": round(rows[dom]["achieved_gbs"] / HBM_PEAK_GBS, 4), "tiling": info}
+            "holograms_per_s": batch / wall, "iter_ms": iter_s * 1e3, "iter_ms_per_hologram": iter_s * 1e3 / batch,
+            "iter_frac_of_hbm_peak_model": round(per_px * batch * n * n / iter_s / 1e9 / HBM_PEAK_GBS, 4),
+            "kernels": {k: {kk: _round(vv) for kk, vv in v.items()} for k, v in rows.items()}, "dominant": dom,
+            "dominant_frac_of_hbm_peak_model": round(rows[dom]["achieved_gbs"] / HBM_PEAK_GBS, 4),
+            "dominant_frac_of_hbm_peak_physical": round(rows[dom]["physical_gbs"] / HBM_PEAK_GBS, 4),
+            "tiling": info}
 
 
 def main():
     opt = parse()
-    d = Dist()
-    _lib.init(d.local_rank if d.world > 1 else int(os.environ.get("SLM_DEVICE", "0")))
+    if opt.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(opt.gpus))
+    rank, world, local_rank = parallel.world()
+    if world > 1 and opt.gpus not in (1, world):
+        print(f"bench.py: --gpus {opt.gpus} but the launcher started {world} ranks; using {world}", file=sys.stderr)
+    group = parallel.Group.from_env()
+    _lib.init(local_rank if world > 1 else int(os.environ.get("SLM_DEVICE", "0")))
     n, bper, iters = opt.size, opt.batch_per_gpu, opt.iters
-    counts = [bper] * d.world
+    counts = [bper] * world
 
-    if d.world > 1:
-        uid = _lib.comm_unique_id() if d.rank == 0 else None
-        uid = d.bcast_bytes(uid)
-        _lib.comm_init(d.world, d.rank, uid)
+    if world > 1:
+        uid = _lib.comm_unique_id() if rank == 0 else None
+        _lib.comm_init(world, rank, group.bcast(uid))
 
     plan = _lib.Plan(_lib.ALGO_GS, bper, n, n, _lib.TGT_F32, False, iters)
-    plan.set_target(targets(d.rank * bper, bper, n))
+    plan.set_target(targets(rank * bper, bper, n))
 
     def step():
         plan.run(iters)
@@ -214,15 +251,15 @@ def main():
     for _ in range(opt.warmup):
         step()
     plan.sync()
-    d.barrier()
+    group.barrier()
     t0 = time.perf_counter()
     for _ in range(opt.steps):
         step()
     plan.sync()
-    d.barrier()
-    elapsed = d.max(time.perf_counter() - t0)
+    group.barrier()
+    elapsed = group.max(time.perf_counter() - t0)
 
-    total_holo = bper * d.world * opt.steps
+    total_holo = bper * world * opt.steps
     value = total_holo / elapsed
     ms_per_step = elapsed / opt.steps * 1e3
 
@@ -231,38 +268,52 @@ def main():
     # sanity: the phases are finite and the error curve decreases
     phase, _, stats, _ = plan.read(expected=False, iters=False)
     ok = bool(np.isfinite(phase).all() and stats[0, iters - 1, 3] < stats[0, 0, 3])
+    ok = all(group.all_gather(ok))
 
-    if d.rank != 0:
+    if rank != 0:
         plan.close()
-        if d.world > 1:
+        if world > 1:
             _lib.comm_destroy()
+        group.close()
         return
 
     prec = info["precision"]  # butterflies / twiddles / exchanges; HBM state is complex64
     key = f"gs_{n}x{n}_b{bper}_it{iters}_{prec}"
     traffic = pmc_traffic(key)
     dr = rows[dom]
+    iter_s = ms_per_step / iters / 1e3
     roofline = {"bound": "hbm", "achieved": round(dr["achieved_gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(dr["achieved_gbs"] / HBM_PEAK_GBS, 4),
                 "traffic": None if traffic is None else traffic.get(dom),
-                "kernel": dom, "avg_us": round(dr["avg_us"], 3), "bytes_per_launch": dr["bytes_per_launch"],
-                "kernels": {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv) for kk, vv in v.items()}
-                            for k, v in rows.items()}}
+                "kernel": dom, "avg_us": round(dr["avg_us"], 3),
+                "bytes_model": "SURVEY.md 8d: GS 68 B/px/iteration = col_main 36 (two column passes 16+16, "
+                               "target 4) + row_main 32 (two row passes); achieved = those bytes per launch / "
+                               "the launch's HIP-event duration",
+                "bytes_per_launch": dr["model_bytes_per_launch"],
+                "physical": {"bytes_per_launch": dr["physical_bytes_per_launch"],
+                             "achieved": round(dr["physical_gbs"], 1),
+                             "frac_physical": round(dr["physical_gbs"] / HBM_PEAK_GBS, 4),
+                             "model": "bytes the fused kernel moves: col_main X 8 + T 4 in, Y 8 out = 20 B/px; "
+                                      "row_main Y 8 in, X 8 out = 16 B/px"},
+                "iteration": {"us": round(iter_s * 1e6, 3),
+                              "frac_model": round(68 * bper * n * n / iter_s / 1e9 / HBM_PEAK_GBS, 4),
+                              "frac_physical": round(36 * bper * n * n / iter_s / 1e9 / HBM_PEAK_GBS, 4)},
+                "kernels": {k: {kk: _round(vv) for kk, vv in v.items()} for k, v in rows.items()}}
     out = {
-        "metric": METRIC, "value": round(value, 3), "unit": "holograms/s", "n_gpus": d.world,
+        "metric": METRIC, "value": round(value, 3), "unit": "holograms/s", "n_gpus": world,
         "steps": opt.steps, "warmup": opt.warmup, "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": prec,
         "data": "synthetic (uniform[0,255) float32 targets, default_rng(1234+b))",
         "config": {"workload": f"GS {n}x{n}, {iters} iterations, {bper} hologram(s) per GPU, float32 target, "
                                "uniform incoming intensity, tolerance 0 (BASELINE.json configs[1])",
-                   "height": n, "width": n, "iters": iters, "batch_per_gpu": bper, "global_batch": bper * d.world,
-                   "parallelism": f"dp{d.world} (independent holograms; RCCL gather of phases to rank 0)",
+                   "height": n, "width": n, "iters": iters, "batch_per_gpu": bper, "global_batch": bper * world,
+                   "parallelism": f"dp{world} (independent holograms; RCCL gather of phases to rank 0)",
                    "storage": "complex64 field, float32 target/phase", "col_tile": info},
         "gs_iter_ms": round(ms_per_step / iters, 5),
         "roofline": roofline,
         "check": "ok" if ok else "FAILED",
     }
-    if d.world == 1 and not opt.no_extra:
+    if world == 1 and not opt.no_extra:
         extra = {"pcie_inclusive": pcie_inclusive(plan, targets(0, bper, n), iters)}
         try:
             extra["gs_4096"] = secondary(4096, 1, 20)
@@ -275,12 +326,14 @@ def main():
         except _lib.SlmError as e:  # pragma: no cover - report, do not hide
             extra["error"] = str(e)
         out["extra"] = extra
-    if d.world == 1 and not opt.no_cpu_baseline:
+    if world == 1 and not opt.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, iters, opt.cpu_sample_seconds)
+        out["cpu_baseline_all_cores"] = cpu_baseline_all_cores(n, iters, opt.cpu_sample_seconds / 2)
     print(json.dumps(out), flush=True)
     plan.close()
-    if d.world > 1:
+    if world > 1:
         _lib.comm_destroy()
+    group.close()
 
 
 if __name__ == "__main__":

@@ -104,9 +104,10 @@ long long slm_plan_kernel_bytes(slm_plan* plan, int kernel_class);
  * (info must hold 8 ints) */
 int slm_plan_info(slm_plan* plan, int* info);
 
-/* Diagnostics: per-workgroup phase timestamps (s_memrealtime, 100 MHz: entry,
- * loads complete, transforms done, stores complete) of the last launch of a
- * kernel class, [batch][workgroups][4]. Needs a library built with
+/* Diagnostics: per-workgroup phase timestamps (s_memrealtime, 100 MHz: tile
+ * start, loads complete, transforms done, stores complete, kernel entry) plus
+ * the wave's HW_ID and XCC_ID, of the last launch of a kernel class,
+ * [batch][workgroups][8]. Needs a library built with
  * -DSLM_TRACE=1 and SLM_TRACE_BUF=1 in the environment at plan creation. */
 int slm_plan_read_trace(slm_plan* plan, int kernel_class, unsigned long long* out);
 

@@ -2,11 +2,10 @@
 pranislav/Spatial_Light_Modulator_Module (src/algorithms.py).
 
 Compute runs only in libslm_hip.so (hand-written gfx950 HIP kernels, loaded
-through ctypes); importing this package loads that library eagerly so that a
-missing build fails at import time rather than silently later.
+through ctypes by ``_lib.load()``). The library is loaded on first use by any
+compute entry point and a missing build raises ImportError there: there is no
+CPU fallback. The package imports no torch; pure host helpers (``parallel``)
+can be imported without the library.
 """
-from . import _lib
 
-_lib.load()
-
-__all__ = ["_lib"]
+__all__ = ["_lib", "algorithms", "parallel"]

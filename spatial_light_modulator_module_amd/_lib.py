@@ -3,6 +3,10 @@
 The shared library is the only compute path of this package: there is no CPU
 fallback. Loading fails loudly when the library has not been built, and every
 compute call raises :class:`SlmError` when no gfx950 device is usable.
+
+No torch: the library links the system ROCm runtime (libamdhip64, librccl).
+A process that also imports PyTorch-ROCm (which bundles its own HIP runtime)
+should import torch first so that one runtime is mapped.
 """
 from __future__ import annotations
 
@@ -87,26 +91,6 @@ SRC_I16 = 1
 _lib = None
 
 
-def _bind_one_hip_runtime():
-    """Keep a single HIP/HSA/RCCL runtime per process.
-
-    PyTorch-ROCm ships its own libamdhip64 / libhsa-runtime64 / librccl under
-    unversioned file names, so a process that loads the system copies (through
-    this library) and then imports torch maps two HIP and two HSA runtimes and
-    aborts in their exit-time destructors. Importing torch first makes this
-    library's NEEDED sonames (libamdhip64.so.7, librccl.so.1) resolve to the
-    copies already mapped. torch is only plumbing here (torch.distributed for
-    multi-process control); SLM_SYSTEM_HIP=1 skips it for torch-free processes
-    that want the system ROCm runtime (they must then never import torch).
-    """
-    if os.environ.get("SLM_SYSTEM_HIP", "0") == "1":
-        return
-    try:
-        import torch  # noqa: F401
-    except ImportError:
-        pass
-
-
 def load() -> ctypes.CDLL:
     """Load libslm_hip.so once; raise ImportError if it was never built."""
     global _lib
@@ -117,7 +101,6 @@ def load() -> ctypes.CDLL:
             f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "(or `make -C spatial_light_modulator_module_amd/csrc`). There is no CPU fallback."
         )
-    _bind_one_hip_runtime()
     lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
     for name, res, args in _SIGNATURES:
         fn = getattr(lib, name)
@@ -270,12 +253,14 @@ class Plan:
                 "col_plan": int(a[6]), "precision": "f64" if a[7] == PRECISION_F64 else "f32"}
 
     def read_trace(self, cls: int) -> np.ndarray:
-        """[batch * workgroups, 4] phase timestamps of the last launch of a
-        kernel class (SLM_TRACE builds with SLM_TRACE_BUF=1; diagnostics)."""
+        """[batch * workgroups, 8] phase timestamps of the last launch of a
+        kernel class (SLM_TRACE builds with SLM_TRACE_BUF=1; diagnostics):
+        tile start, loads done, transforms done, stores done, kernel entry,
+        HW_ID, XCC_ID (kernels.hpp, trace_point)."""
         b, h, w = self.shape
         info = self.info()
         n = info["col_workgroups"] if cls == KERNEL_COL_MAIN else h // info["rows_per_workgroup"]
-        out = np.zeros((b * n, 4), np.uint64)
+        out = np.zeros((b * n, 8), np.uint64)
         check(self._lib.slm_plan_read_trace(self.handle, cls, ptr(out)), "slm_plan_read_trace")
         return out
 

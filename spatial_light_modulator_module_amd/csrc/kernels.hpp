@@ -46,7 +46,7 @@ struct RowParams {
     long long holo;          // elements per hologram (H * W)
     float inv_s;             // 1 / (H * W)
     const void* tw;          // twiddle table for length W (float2 or double2)
-    unsigned long long* trace;  // SLM_TRACE builds: [tile][4] phase timestamps
+    unsigned long long* trace;  // SLM_TRACE builds: [tile][8] phase timestamps (kTraceSlots)
     int B;                   // holograms
     int ntile;               // row groups per hologram (H / rows per workgroup)
 };
@@ -69,7 +69,7 @@ struct ColParams {
     long long holo;          // elements per hologram
     float wa;                // GD white_attention
     const void* tw;          // twiddle table for length H (float2 or double2)
-    unsigned long long* trace;  // SLM_TRACE builds: [tile][4] phase timestamps
+    unsigned long long* trace;  // SLM_TRACE builds: [tile][8] phase timestamps (kTraceSlots)
     int B;                   // holograms
 };
 
@@ -148,21 +148,47 @@ struct ColCfg {
         THREADS >= 64 && THREADS <= 1024 && lds_line(PlanOf<K>::N) * CW * 8 <= 160 * 1024;
 };
 
-// Phase timeline of one workgroup (SLM_TRACE diagnostic builds only):
-// s_memrealtime (100 MHz, chip-wide) at entry, loads complete, transforms
-// done, stores complete.
+// XCD-aware bijective remap: blocks that share (id % 8) — one XCD under the
+// observed round-robin dispatch — get consecutive logical column groups, so
+// the partial 128-B lines of narrow column tiles are shared through one L2.
+// Speed only; correctness does not depend on placement.
+__device__ __forceinline__ int xcd_remap(int id, int n) {
+    const int q = n >> 3, r = n & 7;
+    const int xcd = id & 7, k = id >> 3;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+}
+
+__device__ __forceinline__ int xcd_remap_fwd(int id, int n) { return xcd_remap(id, n); }
+
+// Phase timeline of one workgroup (SLM_TRACE diagnostic builds only), slots
+// [tile][8]: s_memrealtime (100 MHz, chip-wide) at 0 tile start (loads
+// issued), 1 loads complete, 2 transforms done, 3 stores complete, 4 kernel
+// entry (before the twiddle loads); 5 HW_ID and 6 XCC_ID of the wave.
 #ifndef SLM_TRACE
 #define SLM_TRACE 0
 #endif
+constexpr int kTraceSlots = 8;
 __device__ __forceinline__ void trace_point(unsigned long long* tr, long long wgid, int i, bool drain) {
 #if SLM_TRACE
     if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (tr && threadIdx.x == 0) tr[wgid * 4 + i] = __builtin_amdgcn_s_memrealtime();
+    if (tr && threadIdx.x == 0) tr[wgid * kTraceSlots + i] = __builtin_amdgcn_s_memrealtime();
 #else
     (void)tr;
     (void)wgid;
     (void)i;
     (void)drain;
+#endif
+}
+__device__ __forceinline__ void trace_entry(unsigned long long* tr) {
+#if SLM_TRACE
+    if (tr && threadIdx.x == 0 && blockIdx.x < gridDim.x) {
+        const long long wg = xcd_remap_fwd(blockIdx.x, gridDim.x);
+        tr[wg * kTraceSlots + 4] = __builtin_amdgcn_s_memrealtime();
+        tr[wg * kTraceSlots + 5] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+        tr[wg * kTraceSlots + 6] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);
+    }
+#else
+    (void)tr;
 #endif
 }
 
@@ -185,16 +211,6 @@ constexpr int occupancy_wpe(int threads, long long lds_bytes) {
     if (wpe < 1) wpe = 1;
     if (wpe > SLM_MAX_WPE) wpe = SLM_MAX_WPE;
     return SLM_OCC ? (int)wpe : 1;
-}
-
-// XCD-aware bijective remap: blocks that share (id % 8) — one XCD under the
-// observed round-robin dispatch — get consecutive logical column groups, so
-// the partial 128-B lines of narrow column tiles are shared through one L2.
-// Speed only; correctness does not depend on placement.
-__device__ __forceinline__ int xcd_remap(int id, int n) {
-    const int q = n >> 3, r = n & 7;
-    const int xcd = id & 7, k = id >> 3;
-    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
 }
 
 // Internal layout of the iteration state (X, Y, GD field, device target):
@@ -440,6 +456,7 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
     const int lrow = qq * QR + q4;
     const long long bstep = (long long)T * p.H;  // slot m adds m * bstep (blocked layout)
     const LdsLine<X> lds{smem + lrow * LINE};
+    if constexpr (MODE == ROW_GS_MAIN || MODE == ROW_GD_MAIN) trace_entry(p.trace);
     Twiddles<K, C, tw_mode<P, RowCfg<K>::THREADS, K, false>()> tw;
     load_twiddles<K, C>(tw, t, p.tw);
 
@@ -567,6 +584,7 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
     const int t = threadIdx.x / CW;
     constexpr long long kStep = 4LL * T;  // blocked layout: row y = t + T m
     const LdsTile<CW, X> lds{smem, c};
+    if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD) trace_entry(p.trace);
     Twiddles<K, C, tw_mode<P, THREADS, K, true>()> tw;
     load_twiddles<K, C>(tw, t, p.tw);
     constexpr bool kTarget = (MODE == COL_GS_MAIN || MODE == COL_GD_STATS || MODE == COL_GD_GRAD);

@@ -680,8 +680,8 @@ int slm_plan_create(int algo, int batch, int height, int width, int tgt_type, in
     RC(alloc((void**)&p->sum_t2, (size_t)batch * sizeof(double)));
     RC(alloc((void**)&p->ts_part, (size_t)batch * kTsBlocks * 2 * sizeof(double)));
     if (const char* e = std::getenv("SLM_TRACE_BUF"); e && std::atoi(e)) {
-        RC(alloc((void**)&p->trace_col, (size_t)batch * max_nwg * 4 * sizeof(unsigned long long)));
-        RC(alloc((void**)&p->trace_row, (size_t)batch * (height / min_rpw) * 4 * sizeof(unsigned long long)));
+        RC(alloc((void**)&p->trace_col, (size_t)batch * max_nwg * kTraceSlots * sizeof(unsigned long long)));
+        RC(alloc((void**)&p->trace_row, (size_t)batch * (height / min_rpw) * kTraceSlots * sizeof(unsigned long long)));
     }
     *out = p;
     return 0;
@@ -692,7 +692,7 @@ int slm_plan_read_trace(slm_plan* p, int kernel_class, unsigned long long* out) 
     unsigned long long* src = kernel_class == SLM_KERNEL_COL_MAIN ? p->trace_col
                               : kernel_class == SLM_KERNEL_ROW_MAIN ? p->trace_row : nullptr;
     if (!src) return fail(SLM_ERR_STATE, "no trace buffer (set SLM_TRACE_BUF=1 before creating the plan)");
-    const long long n = (long long)p->B * (kernel_class == SLM_KERNEL_COL_MAIN ? p->nwg : p->H / p->rpw) * 4;
+    const long long n = (long long)p->B * (kernel_class == SLM_KERNEL_COL_MAIN ? p->nwg : p->H / p->rpw) * kTraceSlots;
     HIP_TRY(hipStreamSynchronize(p->stream));
     HIP_TRY(hipMemcpy(out, src, n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     return 0;

@@ -4,10 +4,13 @@
 
 The reference runs gerchberg_saxton once per frame (src/generate_hologram_sequence.py:10-31);
 frames are independent, so here they run as batches of holograms in one plan
-(one launch pair per GS iteration for the whole batch), and under
-torch.distributed.run each rank takes a contiguous shard of the frames
-(parallel.shard_range) and writes its own .npy files: no collective touches the
-data path. Output files, names and stdout lines are the reference's.
+(one launch pair per GS iteration for the whole batch), and under a
+one-process-per-GPU launcher (torch.distributed.run or any that sets RANK /
+WORLD_SIZE / MASTER_ADDR / MASTER_PORT) each rank takes a contiguous shard of
+the frames (parallel.shard_range) and writes its own .npy files: no collective
+touches the data path; only the per-frame error lists travel, over the
+torch-free control plane (parallel.Group). Output files, names and stdout lines
+are the reference's.
 """
 from __future__ import annotations
 
@@ -112,12 +115,9 @@ def cli(argv=None, plot=True):
     rank, nranks, _ = parallel.world()
     errors = generate_hologram_sequence(args, rank, nranks)
     if nranks > 1:
-        import torch.distributed as dist
-
-        if not dist.is_initialized():
-            dist.init_process_group("gloo")  # error lists are host objects; the phases went to disk
-        gathered = [None] * nranks
-        dist.all_gather_object(gathered, errors)
+        # error lists are host objects; the phases went to disk
+        with parallel.Group.from_env() as group:
+            gathered = group.all_gather(errors)
         errors = {k: v for part in gathered for k, v in part.items()}
     print()
     if plot and rank == 0:

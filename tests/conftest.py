@@ -1,8 +1,5 @@
-"""Shared pytest configuration.
-
-The package is imported first: loading libslm_hip.so imports torch ahead of
-it (_lib._bind_one_hip_runtime) so the whole process shares one HIP runtime.
-"""
+"""Shared pytest configuration. The package imports no torch; libslm_hip.so is
+loaded here so that a missing build fails the session at once."""
 import os
 import sys
 
@@ -12,7 +9,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-import spatial_light_modulator_module_amd  # noqa: E402,F401  (loads libslm_hip.so first)
+from spatial_light_modulator_module_amd import _lib as _slm_lib  # noqa: E402
+
+_slm_lib.load()
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 

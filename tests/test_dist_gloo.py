@@ -1,26 +1,38 @@
-"""The N > 1 path on CPU: world_size-2 gloo process groups.
+"""The N > 1 path on CPU: world_size-2 (and 3) process groups.
 
 Holograms are independent: ranks take contiguous shards
 (parallel.shard_range), compute with no data-path collective, and only the
-results travel (RCCL send/recv to rank 0 on the GPU box; gloo here). The HIP
-compute is replaced by the float64 oracle in these CPU tests - the sharding,
-gather order, file output and the reference CLI behaviour are what is tested.
+results travel (RCCL send/recv to rank 0 on the GPU box). The host control
+plane is parallel.Group (stdlib TCP, no torch); a gloo process group is run
+beside it as the cross-check. The HIP compute is replaced by the float64
+oracle in these CPU tests - the sharding, gather order, file output and the
+reference CLI behaviour are what is tested. Workers are spawned processes;
+torch is imported only inside the gloo workers.
 """
+import multiprocessing
 import os
-import socket
 
 import numpy as np
 import pytest
-import torch.multiprocessing as mp
 
 from oracle import gs_gd_oracle as orc
 from spatial_light_modulator_module_amd import parallel
 
+_free_port = parallel.free_port
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+
+def _spawn(fn, args, nprocs):
+    """torch.multiprocessing.spawn's contract on the stdlib: fn(rank, *args)."""
+    ctx = multiprocessing.get_context("spawn")
+    procs = [ctx.Process(target=fn, args=(r,) + tuple(args)) for r in range(nprocs)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
 
 
 def oracle_run_gs(targets, loops, tol=0.0, ain=None, initial_phase=None):
@@ -55,33 +67,72 @@ def test_assemble_checks_counts():
 
 def _setup(rank, world, port):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank))
-    import torch.distributed as dist
-
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    return dist
+                      LOCAL_RANK=str(rank), SLM_RDZV_PORT=str(port + 1))
+    return parallel.Group.from_env(timeout=60)
 
 
 def _batch_worker(rank, world, port, targets, loops, out_path):
-    dist = _setup(rank, world, port)
+    group = _setup(rank, world, port)
     mine = parallel.shard_range(len(targets), world, rank)
     phase, _, _, _, _ = oracle_run_gs(targets[mine.start:mine.stop], loops)
-    parts = [None] * world
-    dist.all_gather_object(parts, phase)
+    parts = group.gather(phase)
     if rank == 0:
         full = parallel.assemble(parts, parallel.shard_counts(len(targets), world))
         np.save(out_path, full)
-    dist.barrier()
-    dist.destroy_process_group()
+    t = group.max(float(rank))
+    assert t == world - 1
+    group.barrier()
+    group.close()
 
 
-def test_sharded_batch_equals_single_process(tmp_path):
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_batch_equals_single_process(tmp_path, world):
     rng = np.random.default_rng(3)
     targets = rng.integers(0, 256, size=(5, 64, 64)).astype(np.uint8)
     out = str(tmp_path / "phase.npy")
-    mp.spawn(_batch_worker, args=(2, _free_port(), targets, 4, out), nprocs=2, join=True)
+    _spawn(_batch_worker, (world, _free_port(), targets, 4, out), world)
     want, _, _, _, _ = oracle_run_gs(targets, 4)
     np.testing.assert_array_equal(np.load(out), want)
+
+
+def _control_plane_vs_gloo_worker(rank, world, port, out_dir):
+    """The torch-free star and a gloo process group agree on every collective
+    bench.py and the sequence CLI use (bcast of the RCCL id, all_gather, max)."""
+    group = _setup(rank, world, port)
+    import torch
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    uid = os.urandom(128) if rank == 0 else None
+    got = group.bcast(uid)
+    ref = [uid]
+    dist.broadcast_object_list(ref, src=0)
+    assert got == ref[0] and len(got) == 128
+    obj = {rank: [np.float64(rank) * 0.5, rank]}
+    mine = group.all_gather(obj)
+    theirs = [None] * world
+    dist.all_gather_object(theirs, obj)
+    assert mine == theirs
+    t = torch.tensor([float(rank) + 0.25], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    assert group.max(float(rank) + 0.25) == float(t.item())
+    group.barrier()
+    dist.barrier()
+    np.save(os.path.join(out_dir, f"ok{rank}.npy"), np.array([1]))
+    dist.destroy_process_group()
+    group.close()
+
+
+def test_control_plane_matches_gloo(tmp_path):
+    _spawn(_control_plane_vs_gloo_worker, (2, _free_port(), str(tmp_path)), 2)
+    assert all((tmp_path / f"ok{r}.npy").exists() for r in range(2))
+
+
+def test_group_single_rank_is_local():
+    g = parallel.Group(0, 1)
+    assert g.all_gather("x") == ["x"] and g.bcast(3) == 3 and g.max(2.5) == 2.5
+    g.barrier()
+    g.close()
 
 
 def _make_sequence(root, n):
@@ -98,17 +149,14 @@ def _make_sequence(root, n):
 
 
 def _sequence_worker(rank, world, port, root):
-    _setup(rank, world, port)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), SLM_RDZV_PORT=str(port + 1))
     from spatial_light_modulator_module_amd import generate_hologram_sequence as ghs
 
     os.chdir(root)
     ghs.run_gs = oracle_run_gs  # CPU stand-in for the GPU batch
     errors = ghs.cli(["seq", "-v", "w2", "-ct2pi", "255", "-loops", "3", "-p"], plot=False)
     np.save(os.path.join(root, f"errors_rank{rank}.npy"), np.array([errors[i] for i in sorted(errors)]))
-    import torch.distributed as dist
-
-    dist.barrier()
-    dist.destroy_process_group()
 
 
 def test_sequence_cli_two_ranks_matches_single(tmp_path, monkeypatch):
@@ -119,7 +167,7 @@ def test_sequence_cli_two_ranks_matches_single(tmp_path, monkeypatch):
     for r in (two, one):
         r.mkdir()
         _make_sequence(str(r), n)
-    mp.spawn(_sequence_worker, args=(2, _free_port(), str(two)), nprocs=2, join=True)
+    _spawn(_sequence_worker, (2, _free_port(), str(two)), 2)
 
     monkeypatch.chdir(one)
     monkeypatch.setattr(ghs, "run_gs", oracle_run_gs)

@@ -129,37 +129,53 @@ def test_gd_1024_configs2(gpu):
 @pytest.mark.gpu
 @pytest.mark.timeout(900)
 def test_gs_4096_warm_start_gate(gpu):
-    """North-star shape: 4096^2 GS warm-started from a 30-iteration state, then
-    100 iterations vs the float64 oracle at <= 1e-5 rms (the 100-iteration gate
-    of SURVEY.md 8c; 200 iterations drift to the bar in complex64 state)."""
+    """North-star shape, SURVEY.md 8c protocol: the reference's state after 30
+    cold-start iterations (float64 oracle), then 100 iterations on the GPU vs
+    the oracle at <= 1e-5 rms (the 100-iteration gate; 200 iterations drift to
+    the bar in complex64 state). The float64-butterfly build is reported too."""
     lib = gpu
     n, span = 4096, 100
     t = bench_targets(0, 1, n)
-    _, _, _, info = gs_run(lib, t, 1)
+    phi30, _, _ = fast_f64.gerchberg_saxton_f64(t[0], 30)
+    phi30 = phi30.astype(np.float32)
+    ref, _, ref_err = fast_f64.gerchberg_saxton_f64(t[0], span, initial_phase=phi30)
+    rms = {}
+    for prec in (lib.PRECISION_F64, lib.PRECISION_F32):
+        with lib.Plan(lib.ALGO_GS, 1, n, n, lib.TGT_F32, False, span) as p:
+            p.set_precision(prec)
+            info = p.info()
+            p.set_target(t)
+            p.set_phase(phi30[None])
+            p.run(span)
+            ph, _, stats, _ = p.read(expected=False)
+        rms[info["precision"]] = orc.phase_rms(ph[0], ref)
+        np.testing.assert_allclose(stats[0, :span, 3], ref_err, rtol=1e-4)
     assert (info["row_plan"], info["col_plan"], info["col_cw"]) == (13, 13, 2), info
-    ph30, _, _, _ = gs_run(lib, t, 30)  # any warmed state serves (the GS state is angle(A) only)
-    ph, _, stats, _ = gs_run(lib, t, span, ph30)
-    ref, _, ref_err = fast_f64.gerchberg_saxton_f64(t[0], span, initial_phase=ph30[0])
-    rms = orc.phase_rms(ph[0], ref)
-    print(f"[parity] 4096^2 warm-start 30+{span}: phase rms {rms:.3e}")
-    assert rms < PHASE_RMS_TOL
-    np.testing.assert_allclose(stats[0, :span, 3], ref_err, rtol=1e-4)
+    print(f"[parity] 4096^2 warm-start 30+{span}: phase rms f32 {rms['f32']:.3e}, f64 butterflies {rms['f64']:.3e}")
+    assert rms["f32"] < PHASE_RMS_TOL
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cw", [8, 16])
 def test_column_tile_widths_bitwise(gpu, cw):
     """512- and 1024-thread column workgroups (cw x 64 threads on the wide 1024
-    plan) give the bits of the default 4-column tiles, run after run: the LDS
-    exchange race of 6e0b072 showed up as ~1.5 % of launches differing here."""
+    plan) give the phases of the default 4-column tiles bit for bit, run after
+    run: the LDS exchange race of 6e0b072 showed up as ~1.5 % of launches
+    differing here. (The error sums are reduced per column panel, so their
+    rounding follows the tile width: equal to 1e-12, and bitwise run to run.)"""
     lib = gpu
     t = bench_targets(0, 4, 1024)
     phi = np.random.default_rng(cw).uniform(-np.pi, np.pi, t.shape).astype(np.float32)
     ref = gs_run(lib, t, 40, phi)
     assert ref[3]["col_cw"] == 4 and ref[3]["col_plan"] == 5
     with plan_env(SLM_COL_CW=cw):
+        first = None
         for _ in range(3):
             ph, e, stats, info = gs_run(lib, t, 40, phi)
             assert info["col_cw"] == cw and info["col_threads"] == cw * 64
             np.testing.assert_array_equal(ph, ref[0])
-            np.testing.assert_array_equal(stats, ref[2])
+            np.testing.assert_array_equal(e, ref[1])
+            np.testing.assert_allclose(stats, ref[2], rtol=1e-12)
+            if first is None:
+                first = stats
+            np.testing.assert_array_equal(stats, first)
