@@ -96,6 +96,16 @@ int slm_plan_sync(slm_plan* plan);
 int slm_plan_read(slm_plan* plan, float* phase, float* expected, double* stats, int* iters);
 /* norm [batch] and sum T^2 [batch] as reduced on the device */
 int slm_plan_read_target_stats(slm_plan* plan, double* norm, double* sum_t2);
+/* Override norm = max(T) and sum T^2 per hologram with values the caller
+ * computed in float64 from its own target (np.amax(demanded_output),
+ * src/algorithms.py:23, and the constant term of error_f :161-162): a
+ * float64 target keeps them exact although the device copy of T is float32.
+ * Call after slm_plan_set_target. */
+int slm_plan_set_target_stats(slm_plan* plan, const double* norm, const double* sum_t2);
+/* GD state x [batch][h][w] complex64 (interleaved re, im) after the last run:
+ * the field a chunked run continues from with slm_plan_set_field (GIF frames,
+ * src/algorithms.py:94-101). */
+int slm_plan_read_field(slm_plan* plan, float* field);
 /* algorithmic HBM bytes moved by one launch of a kernel class */
 long long slm_plan_kernel_bytes(slm_plan* plan, int kernel_class);
 /* info[0] = column tile width, info[1] = column workgroups per hologram,
@@ -154,6 +164,25 @@ int slm_trap_frames(int batch, int height, int width, const int* ys, const int* 
                     double ct2pi, int rule, double* phase_out, unsigned char* frame_out);
 int slm_quantize(const void* src, int src_type, const double* mask, int batch, int height, int width, double ct2pi,
                  int rule, unsigned char* out);
+
+/* ---- CLI post-processing ------------------------------
+ * slm_transform_hologram -> transform_hologram(hologram, args)
+ *                           src/generate_hologram.py:82-87: deflect_hologram
+ *                           (:178-181 with wavefront_correction.deflect_2pi,
+ *                           src/wavefront_correction.py:440-449) and add_lens
+ *                           (:184-203, lens() stored as uint8). float64,
+ *                           reference operation order, bit for bit.
+ * holo_in [height][width] float64 or NULL (zeros); params = {sin(y_angle u),
+ * sin(x_angle u), 2 pi px_distance / wavelength, 2 pi focal / wavelength,
+ * focal, px_distance} as the reference computes them on the host.
+ * slm_fft2_intensity     -> show_expected_outcome's |fft2(exp(1j h))|^2
+ *                           (src/generate_hologram.py:24-34) on the plan
+ *                           kernels (complex64), row-major float32 out.   */
+#define SLM_TRANSFORM_DEFLECT 1
+#define SLM_TRANSFORM_LENS 2
+int slm_transform_hologram(const double* holo_in, int height, int width, int flags, const double* params,
+                           double* holo_out);
+int slm_fft2_intensity(const float* phase, int batch, int height, int width, float* intensity_out);
 
 #ifdef __cplusplus
 }

@@ -67,6 +67,8 @@ _SIGNATURES = [
     ("slm_plan_sync", _c_int, [_vp]),
     ("slm_plan_read", _c_int, [_vp, _vp, _vp, _vp, _vp]),
     ("slm_plan_read_target_stats", _c_int, [_vp, _vp, _vp]),
+    ("slm_plan_set_target_stats", _c_int, [_vp, _vp, _vp]),
+    ("slm_plan_read_field", _c_int, [_vp, _vp]),
     ("slm_plan_kernel_bytes", ctypes.c_longlong, [_vp, _c_int]),
     ("slm_plan_info", _c_int, [_vp, _vp]),
     ("slm_plan_read_trace", _c_int, [_vp, _c_int, _vp]),
@@ -81,7 +83,12 @@ _SIGNATURES = [
     ("slm_trap_frames", _c_int,
      [_c_int, _c_int, _c_int, _vp, _vp, _vp, _c_double, _c_int, _vp, _vp]),
     ("slm_quantize", _c_int, [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_double, _c_int, _vp]),
+    ("slm_transform_hologram", _c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp]),
+    ("slm_fft2_intensity", _c_int, [_vp, _c_int, _c_int, _c_int, _vp]),
 ]
+
+TRANSFORM_DEFLECT = 1
+TRANSFORM_LENS = 2
 
 QUANT_ASTYPE = 0
 QUANT_PIL = 1
@@ -242,6 +249,17 @@ class Plan:
         check(self._lib.slm_plan_read_target_stats(self.handle, ptr(norm), ptr(st2)), "slm_plan_read_target_stats")
         return norm, st2
 
+    def set_target_stats(self, norm, sum_t2) -> None:
+        n = np.ascontiguousarray(norm, dtype=np.float64).reshape(self.batch)
+        s = np.ascontiguousarray(sum_t2, dtype=np.float64).reshape(self.batch)
+        check(self._lib.slm_plan_set_target_stats(self.handle, ptr(n), ptr(s)), "slm_plan_set_target_stats")
+
+    def read_field(self) -> np.ndarray:
+        """GD state x [batch][h][w] complex64 after the last run."""
+        out = np.empty(self.shape, np.complex64)
+        check(self._lib.slm_plan_read_field(self.handle, ptr(out.view(np.float32))), "slm_plan_read_field")
+        return out
+
     def kernel_bytes(self, cls: int) -> int:
         return int(self._lib.slm_plan_kernel_bytes(self.handle, cls))
 
@@ -279,6 +297,38 @@ def fft2(x: np.ndarray, inverse: bool = False) -> np.ndarray:
     out = np.empty_like(a)
     check(load().slm_fft2(ptr(a.view(np.float32)), ptr(out.view(np.float32)), b, h, w, int(bool(inverse))),
           "slm_fft2")
+    return out
+
+
+def transform_hologram(hologram, height, width, deflect_params=None, lens_params=None):
+    """deflect / lens post-processing of src/generate_hologram.py:82-87 on the
+    GPU (slm_transform_hologram). hologram float64 [h][w] or None (zeros);
+    deflect_params = (sin(y u), sin(x u), 2 pi px / wl); lens_params =
+    (2 pi f / wl, f, px)."""
+    flags = 0
+    params = np.zeros(6, np.float64)
+    if deflect_params is not None:
+        flags |= TRANSFORM_DEFLECT
+        params[0:3] = deflect_params
+    if lens_params is not None:
+        flags |= TRANSFORM_LENS
+        params[3:6] = lens_params
+    src = None if hologram is None else np.ascontiguousarray(hologram, dtype=np.float64).reshape(height, width)
+    out = np.empty((height, width), np.float64)
+    init()
+    check(load().slm_transform_hologram(ptr(src), height, width, flags, ptr(params), ptr(out)),
+          "slm_transform_hologram")
+    return out
+
+
+def fft2_intensity(phase) -> np.ndarray:
+    """|fft2(exp(1j phase))|^2 on the GPU (float32), phase [..., H, W]."""
+    a = np.ascontiguousarray(phase, dtype=np.float32)
+    h, w = a.shape[-2:]
+    b = int(np.prod(a.shape[:-2])) if a.ndim > 2 else 1
+    out = np.empty(a.shape, np.float32)
+    init()
+    check(load().slm_fft2_intensity(ptr(a), b, h, w, ptr(out)), "slm_fft2_intensity")
     return out
 
 

@@ -10,9 +10,13 @@ iteration arithmetic runs in libslm_hip.so; this module only prepares inputs
 (dtype rules, initial guesses) and formats results.
 
 Differences that remain: image sides must be one of
-SUPPORTED_LENGTHS, and the loop state lives in complex64 in HBM (butterflies
-and twiddles in float64 by default), so phases match the float64 reference to
-<= 1e-5 rms under the warm-start protocol of SURVEY.md 8c, not bitwise.
+SUPPORTED_LENGTHS, and the loop state lives in complex64 in HBM with float32
+butterflies, twiddles and projections by default (float64 butterflies per plan
+with Plan.set_precision or $SLM_PRECISION=f64), so phases match the float64
+reference to <= 1e-5 rms under the warm-start protocol of SURVEY.md 8c (float32
+margins measured in DESIGN.md section 5: 4.0e-6..6.0e-6 at 256^2-1024^2), not
+bitwise. A float64 target is carried as float32 on the device, with its max
+and sum of squares (the error's constant terms) kept exact in float64.
 """
 from __future__ import annotations
 
@@ -49,6 +53,17 @@ def target_for_device(demanded_output) -> tuple[np.ndarray, int]:
     if t.dtype == np.uint8:
         return np.ascontiguousarray(t), TGT_U8
     return np.ascontiguousarray(t, dtype=np.float32), TGT_F32
+
+
+def _exact_target_stats(plan, t):
+    """A target that float32 does not hold exactly (float64, wide integers)
+    keeps norm = np.amax(T) (src/algorithms.py:23) and sum T^2 (error_f's
+    constant term, :161-162) in float64; the cross term sum E*T uses the
+    float32 device copy (relative effect <= 2^-24 per pixel)."""
+    if t.dtype in (np.uint8, np.float32, np.float16) or (t.dtype.kind in "iu" and t.dtype.itemsize <= 2):
+        return
+    tf = t.astype(np.float64).reshape(plan.batch, -1)
+    plan.set_target_stats(tf.max(axis=1), np.einsum("ij,ij->i", tf, tf))
 
 
 def incoming_amplitude(args, shape) -> np.ndarray | None:
@@ -148,6 +163,7 @@ def run_gs(targets, loops, tol=0.0, ain=None, initial_phase=None):
     b, h, w = tdev.shape
     plan = get_plan(ALGO_GS, b, h, w, tt, ain is not None, loops)
     plan.set_target(tdev)
+    _exact_target_stats(plan, t)
     if ain is not None:
         plan.set_ain(ain)
     plan.set_phase(initial_phase)
@@ -174,12 +190,13 @@ def _collect(plan, phase, e, stats, iters, loops, checked):
     return phase, e, errs, norm, np.array(maxes)
 
 
-def run_gd(targets, loops, rates, white_attention, tol=0.0, ain=None, initial_field=None):
+def run_gd(targets, loops, rates, white_attention, tol=0.0, ain=None, initial_field=None, return_field=False):
     t = np.asarray(targets)
     tdev, tt = target_for_device(t)
     b, h, w = tdev.shape
     plan = get_plan(ALGO_GD, b, h, w, tt, ain is not None, loops)
     plan.set_target(tdev)
+    _exact_target_stats(plan, t)
     if ain is not None:
         plan.set_ain(ain)
     plan.set_field(initial_field)
@@ -192,7 +209,8 @@ def run_gd(targets, loops, rates, white_attention, tol=0.0, ain=None, initial_fi
             plan.run(loops, tol, True, white_attention)
             phase, e, stats, iters = plan.read()
             checked = True
-    return _collect(plan, phase, e, stats, iters, loops, checked)
+    out = _collect(plan, phase, e, stats, iters, loops, checked)
+    return out + (plan.read_field(),) if return_field else out
 
 
 def hologram_from(phase):
@@ -236,10 +254,18 @@ def _iterations_allowed(args):
 
 
 def _gif_frame(args, kind, phase, expected, i):
+    """add_gif_image (src/algorithms.py:52-57) for GS; the GD frame of
+    src/algorithms.py:94-101 (complex_to_real_phase of x/|x|, :175-176) when
+    `phase` is the GD field."""
     from PIL import Image
 
     if args.gif_type == "h":
-        img = Image.fromarray((hologram_from(phase) + np.pi) * args.correspond_to2pi / (2 * np.pi))
+        if kind == "gd":
+            ang = np.angle(phase.astype(np.complex128))
+        else:
+            ang = hologram_from(phase)
+        img = Image.fromarray((ang + np.pi) * args.correspond_to2pi / (2 * np.pi)
+                              if kind == "gs" else (ang + np.pi) / (2 * np.pi) * args.correspond_to2pi)
     elif args.gif_type == "i":
         img = Image.fromarray(expected)
     else:
@@ -318,9 +344,9 @@ def gradient_descent(demanded_output, args):
         raise UnboundLocalError("local variable 'output' referenced before assignment")
     if args.unsettle and int(round(args.max_loops / (args.unsettle + 1))) == 0:
         raise ZeroDivisionError("integer division or modulo by zero")
-    if args.gif:
-        raise NotImplementedError("gif frames are supported for gerchberg_saxton only")
     rates, after = learning_rates(args.learning_rate, args.max_loops, args.unsettle)
+    if args.gif:
+        return _gradient_descent_gif(t, args, ain, field, rates, after)
     phase, e, errs, norm, emax = run_gd(t[None], args.max_loops, rates, float(args.white_attention), tol, ain,
                                         None if field is None else field[None])
     error_evolution = errs[0]
@@ -333,3 +359,33 @@ def gradient_descent(demanded_output, args):
     hologram = hologram_from(phase[0])
     output = expected_from(e[0], norm[0], emax[0])
     return hologram, output, error_evolution
+
+
+def _gradient_descent_gif(t, args, ain, field, rates, after):
+    """GD with GIF frames (src/algorithms.py:94-101): warm-started chunks that
+    end on every frame iteration; the GD state is the complex field x, read
+    back after each chunk (slm_plan_read_field) and handed to the next with the
+    matching slice of the learning-rate schedule."""
+    loops, tol, skip = args.max_loops, args.tolerance, args.gif_skip
+    error_evolution = []
+    i = 0
+    x = None if field is None else field[None]
+    while i < loops:
+        step = 1 if i % skip == 0 else min(skip - i % skip, loops - i)
+        ph, e, errs, norm, emax, xf = run_gd(t[None], step, rates[i:i + step], float(args.white_attention), tol,
+                                             ain, x, return_field=True)
+        x = xf
+        error_evolution += errs[0]
+        i += len(errs[0])
+        output = expected_from(e[0], norm[0], emax[0])
+        if (i - 1) % skip == 0:
+            _gif_frame(args, "gd", xf[0], output, i - 1)
+        if len(errs[0]) < step or not (error_evolution[-1] > tol):
+            break
+    n = len(error_evolution)
+    args.learning_rate = float(after[n]) if args.unsettle else args.learning_rate
+    _print_loops(n, loops)
+    if args.print_info:
+        print()
+        printout(error_evolution[-1], n, error_evolution, args.plot_error)
+    return hologram_from(ph[0]), output, error_evolution

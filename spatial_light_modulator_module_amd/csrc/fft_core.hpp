@@ -235,32 +235,38 @@ struct Dft<16, INV, C> {
 
 // ------------------------------------------------------------------------
 // LDS views (complex64). A pass writes output element o and reads element
-// t + T m of the line; padding one slot per 16 keeps the strided first-pass
-// writes off a single bank.
+// t + T m of a line; padding one slot per 16 keeps the strided first-pass
+// writes off a single bank. A thread may carry L lines (argument l), which
+// share its twiddles and its exchange barriers.
 // ------------------------------------------------------------------------
 // X = float2 or double2: the element type of the exchange (float64 exchanges
 // avoid two conversions per element and pass where the LDS budget allows).
 template <class X>
-struct LdsLine {  // one transform line per thread group (row kernels)
+struct LdsLine {  // per-line LDS regions `stride` apart (row kernels)
     X* base;
+    int stride = 0;
     template <class C>
-    __device__ __forceinline__ void store(int o, C v) const { base[o + (o >> 4)] = mk<X>(v.x, v.y); }
+    __device__ __forceinline__ void store(int l, int o, C v) const {
+        base[l * stride + o + (o >> 4)] = mk<X>(v.x, v.y);
+    }
     template <class C>
-    __device__ __forceinline__ C load(int o) const {
-        const X v = base[o + (o >> 4)];
+    __device__ __forceinline__ C load(int l, int o) const {
+        const X v = base[l * stride + o + (o >> 4)];
         return mk<C>(v.x, v.y);
     }
 };
 
 template <int CW, class X>
-struct LdsTile {  // CW interleaved columns (column kernels): [o][c]
+struct LdsTile {  // CW interleaved columns (column kernels): [o][c]; the thread's lines are c + l
     X* base;
     int c;
     template <class C>
-    __device__ __forceinline__ void store(int o, C v) const { base[(o + (o >> 4)) * CW + c] = mk<X>(v.x, v.y); }
+    __device__ __forceinline__ void store(int l, int o, C v) const {
+        base[(o + (o >> 4)) * CW + c + l] = mk<X>(v.x, v.y);
+    }
     template <class C>
-    __device__ __forceinline__ C load(int o) const {
-        const X v = base[(o + (o >> 4)) * CW + c];
+    __device__ __forceinline__ C load(int l, int o) const {
+        const X v = base[(o + (o >> 4)) * CW + c + l];
         return mk<C>(v.x, v.y);
     }
 };
@@ -489,9 +495,9 @@ __device__ __forceinline__ To cv(From a) {
     return mk<To>((Scalar<To>)a.x, (Scalar<To>)a.y);
 }
 
-template <int N, int E, bool INV, int Ns, int TwOff, int RegOff, int PowOff, class C, class V, class Lds, class Tw,
-          class Sink, int R, int... Rest>
-__device__ __forceinline__ void stockham_from(V (&v)[E], int t, const Tw& tw, const Lds& lds, Sink& sink) {
+template <int N, int E, int L, bool INV, int Ns, int TwOff, int RegOff, int PowOff, class C, class V, class Lds,
+          class Tw, class Sink, int R, int... Rest>
+__device__ __forceinline__ void stockham_from(V (&v)[L][E], int t, const Tw& tw, const Lds& lds, Sink& sink) {
     constexpr int T = N / E;
     constexpr int NB = E / R;
     static_assert(E % R == 0, "radix must divide elements per thread");
@@ -499,41 +505,47 @@ __device__ __forceinline__ void stockham_from(V (&v)[E], int t, const Tw& tw, co
         constexpr int k = decltype(kc)::value;
         const int b = t + k * T;
         const int j = (Ns == 1) ? 0 : (b % Ns);
-        C u[R];
-        static_for<R>([&](auto rc) {
-            constexpr int r = decltype(rc)::value;
-            u[r] = cv<C>(v[k + r * NB]);
-        });
-        if constexpr (Ns > 1) tw.template apply<TwOff, RegOff, PowOff, R, Ns, INV>(u, k, j);
-        Dft<R, INV, C>::run(u);
-        if constexpr (sizeof...(Rest) == 0) {
-            // last pass: Ns * R == N, so b < Ns and output r belongs in slot k + r NB
-            sink(kc, u);
-        } else {
-            const int o = (b / Ns) * Ns * R + j;
+        static_for<L>([&](auto lc) {
+            constexpr int l = decltype(lc)::value;
+            C u[R];
             static_for<R>([&](auto rc) {
                 constexpr int r = decltype(rc)::value;
-                lds.store(o + r * Ns, u[r]);
+                u[r] = cv<C>(v[l][k + r * NB]);
             });
-        }
+            if constexpr (Ns > 1) tw.template apply<TwOff, RegOff, PowOff, R, Ns, INV>(u, k, j);
+            Dft<R, INV, C>::run(u);
+            if constexpr (sizeof...(Rest) == 0) {
+                // last pass: Ns * R == N, so b < Ns and output r belongs in slot k + r NB
+                sink(lc, kc, u);
+            } else {
+                const int o = (b / Ns) * Ns * R + j;
+                static_for<R>([&](auto rc) {
+                    constexpr int r = decltype(rc)::value;
+                    lds.store(l, o + r * Ns, u[r]);
+                });
+            }
+        });
 #if SLM_GROUP_FENCE
         // keep butterfly groups apart in the schedule: bounds the live registers
-        // to about one group's worth in the compute type
+        // to about one group's worth (per line) in the compute type
         __builtin_amdgcn_sched_barrier(0);
 #endif
     });
     if constexpr (sizeof...(Rest) > 0) {
         exchange_barrier();
-        static_for<E>([&](auto mc) {
-            constexpr int m = decltype(mc)::value;
-            v[m] = lds.template load<V>(t + m * T);
+        static_for<L>([&](auto lc) {
+            constexpr int l = decltype(lc)::value;
+            static_for<E>([&](auto mc) {
+                constexpr int m = decltype(mc)::value;
+                v[l][m] = lds.template load<V>(l, t + m * T);
+            });
         });
         exchange_barrier();
         constexpr int kNextReg = RegOff + (Ns > 1 ? NB * (R - 1) : 0);
         constexpr int kNextOff = TwOff + (Ns > 1 ? (R - 1) * Ns : 0);
         constexpr int kNextPow = PowOff + (Ns > 1 ? NB : 0);
-        stockham_from<N, E, INV, Ns * R, kNextOff, kNextReg, kNextPow, C, V, Lds, Tw, Sink, Rest...>(v, t, tw, lds,
-                                                                                                   sink);
+        stockham_from<N, E, L, INV, Ns * R, kNextOff, kNextReg, kNextPow, C, V, Lds, Tw, Sink, Rest...>(v, t, tw, lds,
+                                                                                                      sink);
     }
 }
 
@@ -555,22 +567,22 @@ template <int K>
 constexpr bool kLaunder = PlanOf<K>::E >= 16;
 
 // whole transform, starting at pass 0
-template <int K, bool INV, class C, class V, class Lds, class Tw, class Sink, int... Rs>
-__device__ __forceinline__ void stockham_all(V (&v)[PlanOf<K>::E], int t, const Tw& tw0, const Lds& lds, Sink& sink,
-                                             IntList<Rs...>) {
+template <int K, bool INV, class C, int L, class V, class Lds, class Tw, class Sink, int... Rs>
+__device__ __forceinline__ void stockham_all(V (&v)[L][PlanOf<K>::E], int t, const Tw& tw0, const Lds& lds,
+                                             Sink& sink, IntList<Rs...>) {
     Tw tw = tw0;
     if constexpr (kLaunder<K>) tw.launder();
-    stockham_from<PlanOf<K>::N, PlanOf<K>::E, INV, 1, 0, 0, 0, C, V, Lds, Tw, Sink, Rs...>(v, t, tw, lds, sink);
+    stockham_from<PlanOf<K>::N, PlanOf<K>::E, L, INV, 1, 0, 0, 0, C, V, Lds, Tw, Sink, Rs...>(v, t, tw, lds, sink);
 }
 // passes 1.. of a transform whose first pass already wrote the LDS line
 // (pass 0 has no twiddles, so every twiddle offset is still 0 here)
-template <int K, bool INV, class C, class V, class Lds, class Tw, class Sink, int R0, int... Rs>
-__device__ __forceinline__ void stockham_after_first(V (&v)[PlanOf<K>::E], int t, const Tw& tw0, const Lds& lds,
+template <int K, bool INV, class C, int L, class V, class Lds, class Tw, class Sink, int R0, int... Rs>
+__device__ __forceinline__ void stockham_after_first(V (&v)[L][PlanOf<K>::E], int t, const Tw& tw0, const Lds& lds,
                                                      Sink& sink, IntList<R0, Rs...>) {
     static_assert(sizeof...(Rs) > 0, "fused transforms need at least two passes");
     Tw tw = tw0;
     if constexpr (kLaunder<K>) tw.launder();
-    stockham_from<PlanOf<K>::N, PlanOf<K>::E, INV, R0, 0, 0, 0, C, V, Lds, Tw, Sink, Rs...>(v, t, tw, lds, sink);
+    stockham_from<PlanOf<K>::N, PlanOf<K>::E, L, INV, R0, 0, 0, 0, C, V, Lds, Tw, Sink, Rs...>(v, t, tw, lds, sink);
 }
 
 template <int... Rs>
@@ -579,76 +591,82 @@ template <int... Rs>
 constexpr int last_radix(IntList<Rs...>) { return LastOf<Rs...>::value; }
 
 // Writes the last pass back to the slots.
-template <int E, class V>
+template <int L, int E, class V>
 struct WriteBack {
-    V (&v)[E];
-    template <class KC, class C, int R>
-    __device__ __forceinline__ void operator()(KC, C (&u)[R]) const {
-        constexpr int k = KC::value, NB = E / R;
+    V (&v)[L][E];
+    template <class LC, class KC, class C, int R>
+    __device__ __forceinline__ void operator()(LC, KC, C (&u)[R]) const {
+        constexpr int l = LC::value, k = KC::value, NB = E / R;
         static_for<R>([&](auto rc) {
             constexpr int r = decltype(rc)::value;
-            v[k + r * NB] = cv<V>(u[r]);
+            v[l][k + r * NB] = cv<V>(u[r]);
         });
     }
 };
 
-// Transform one line held in the slot layout. Every thread of the workgroup
+// Transform L lines held in the slot layout. Every thread of the workgroup
 // must call these (they contain workgroup barriers).
-template <int K, bool INV, class C, class V, class Lds, class Tw>
-__device__ __forceinline__ void fft_line(V (&v)[PlanOf<K>::E], int t, const Tw& tw, const Lds& lds) {
-    WriteBack<PlanOf<K>::E, V> wb{v};
+template <int K, bool INV, class C, int L, class V, class Lds, class Tw>
+__device__ __forceinline__ void fft_line(V (&v)[L][PlanOf<K>::E], int t, const Tw& tw, const Lds& lds) {
+    WriteBack<L, PlanOf<K>::E, V> wb{v};
     stockham_all<K, INV, C>(v, t, tw, lds, wb, RadicesOf<K>{});
 }
 
-// Transform, then epi(slot m, C& z) on every output in the compute type, then
-// write back.
-template <int K, bool INV, class C, class V, class Lds, class Tw, class Epi>
-__device__ __forceinline__ void fft_line_epi(V (&v)[PlanOf<K>::E], int t, const Tw& tw, const Lds& lds, Epi&& epi) {
+// Transform, then epi(line l, slot m, C& z) on every output in the compute
+// type, then write back.
+template <int K, bool INV, class C, int L, class V, class Lds, class Tw, class Epi>
+__device__ __forceinline__ void fft_line_epi(V (&v)[L][PlanOf<K>::E], int t, const Tw& tw, const Lds& lds,
+                                             Epi&& epi) {
     constexpr int E = PlanOf<K>::E;
-    auto sink = [&](auto kc, auto& u) {
+    auto sink = [&](auto lc, auto kc, auto& u) {
+        constexpr int l = decltype(lc)::value;
         constexpr int k = decltype(kc)::value;
         constexpr int R = sizeof(u) / sizeof(u[0]);
         constexpr int NB = E / R;
         static_for<R>([&](auto rc) {
             constexpr int r = decltype(rc)::value;
-            epi(k + r * NB, u[r]);
-            v[k + r * NB] = cv<V>(u[r]);
+            epi(l, k + r * NB, u[r]);
+            v[l][k + r * NB] = cv<V>(u[r]);
         });
     };
     stockham_all<K, INV, C>(v, t, tw, lds, sink, RadicesOf<K>{});
 }
 
-// Transform (INV1), epi(slot m, C& z) on every output, transform (INV2).
-template <int K, bool INV1, bool INV2, class C, class V, class Lds, class Tw, class Epi>
-__device__ __forceinline__ void fft_pair(V (&v)[PlanOf<K>::E], int t, const Tw& tw, const Lds& lds, Epi&& epi) {
+// Transform (INV1), epi(line l, slot m, C& z) on every output, transform (INV2).
+template <int K, bool INV1, bool INV2, class C, int L, class V, class Lds, class Tw, class Epi>
+__device__ __forceinline__ void fft_pair(V (&v)[L][PlanOf<K>::E], int t, const Tw& tw, const Lds& lds, Epi&& epi) {
     constexpr int E = PlanOf<K>::E;
     constexpr int T = PlanOf<K>::T;
     constexpr int R0 = first_radix(RadicesOf<K>{});
     constexpr int RL = last_radix(RadicesOf<K>{});
     if constexpr (SLM_FUSE_PAIR && R0 == RL && kPlans[K].npass > 1) {
         // group k of the last pass is group k of the next transform's first pass
-        auto sink = [&](auto kc, auto& u) {
+        auto sink = [&](auto lc, auto kc, auto& u) {
+            constexpr int l = decltype(lc)::value;
             constexpr int k = decltype(kc)::value;
             constexpr int NB = E / RL;
             static_for<RL>([&](auto rc) {
                 constexpr int r = decltype(rc)::value;
-                epi(k + r * NB, u[r]);
+                epi(l, k + r * NB, u[r]);
             });
             Dft<RL, INV2, C>::run(u);  // first pass: Ns = 1, no twiddles
             const int o = (t + k * T) * RL;
             static_for<RL>([&](auto rc) {
                 constexpr int r = decltype(rc)::value;
-                lds.store(o + r, u[r]);
+                lds.store(l, o + r, u[r]);
             });
         };
         stockham_all<K, INV1, C>(v, t, tw, lds, sink, RadicesOf<K>{});
         exchange_barrier();
-        static_for<E>([&](auto mc) {
-            constexpr int m = decltype(mc)::value;
-            v[m] = lds.template load<V>(t + m * T);
+        static_for<L>([&](auto lc) {
+            constexpr int l = decltype(lc)::value;
+            static_for<E>([&](auto mc) {
+                constexpr int m = decltype(mc)::value;
+                v[l][m] = lds.template load<V>(l, t + m * T);
+            });
         });
         exchange_barrier();
-        WriteBack<E, V> wb{v};
+        WriteBack<L, E, V> wb{v};
         stockham_after_first<K, INV2, C>(v, t, tw, lds, wb, RadicesOf<K>{});
     } else {
         fft_line_epi<K, INV1, C>(v, t, tw, lds, epi);

@@ -1,5 +1,16 @@
-// SLM frame kernels: single-trap holograms and the
-// quantisation of phase (+ correction mask) to the SLM's 8-bit levels.
+// SLM frame kernels: single-trap holograms, the
+// quantisation of phase (+ correction mask) to the SLM's 8-bit levels, and the
+// CLI's hologram post-processing (deflecting ramp + lens).
+//
+//   transform_hologram src/generate_hologram.py:82-87, 178-203 and
+//                      src/wavefront_correction.py:440-449
+//                        deflect: (h + (c (sin(y u) i + sin(x u) j)) % 2pi) % 2pi
+//                        lens:    (h + uint8(phase_shift(r) % 2pi)) % 2pi
+//                      in float64 with the reference's operation order and no
+//                      contraction (this file builds with -ffp-contract=off), so the result is
+//                      the reference's bit for bit; the two sin() values and
+//                      the constants are computed on the host as the
+//                      reference computes them (Python floats).
 //
 //   update_hologram   src/move_traps.py:64-68      np.angle(ifft2(255 at (y, x)))
 //   display_hologram  src/move_traps.py:135-139    ((h + mask) % 2pi * ct2pi / 2pi).astype(uint8)
@@ -49,6 +60,41 @@ __device__ __forceinline__ uint8_t pil_f_to_l(double v) {
 __device__ __forceinline__ uint8_t quantize(double h, double m, double ct2pi, int rule) {
     if (rule == SLM_QUANT_ASTYPE) return astype_u8(py_mod(h + m, kTwoPi) * ct2pi / kTwoPi);
     return pil_f_to_l(py_mod(h + m, kTwoPi) / kTwoPi * ct2pi);
+}
+
+struct TransformParams {
+    const double* in;  // [H][W] hologram or nullptr (zeros, the CLI's analytical case)
+    double* out;
+    int H, W;
+    int deflect, lens;
+    double sin_y, sin_x, ramp_c;  // np.sin(y_angle * u), np.sin(x_angle * u), 2 pi px / wavelength
+    double lens_c, focal, px;     // 2 pi focal / wavelength, focal length, pixel pitch
+};
+
+__global__ void __launch_bounds__(256) transform_kernel(TransformParams p) {
+    const long long n = (long long)p.H * p.W;
+    for (long long k = blockIdx.x * 256LL + threadIdx.x; k < n; k += (long long)gridDim.x * 256) {
+        const int i = (int)(k / p.W), j = (int)(k - (long long)i * p.W);
+        double h = p.in ? p.in[k] : 0.0;
+        if (p.deflect) {
+            // deflect_2pi: const * (sin(y u) * i + sin(x u) * j) % 2pi; then (h + ramp) % 2pi
+            const double s = __dadd_rn(__dmul_rn(p.sin_y, (double)i), __dmul_rn(p.sin_x, (double)j));
+            const double ramp = py_mod(__dmul_rn(p.ramp_c, s), kTwoPi);
+            h = py_mod(__dadd_rn(h, ramp), kTwoPi);
+        }
+        if (p.lens) {
+            // lens(): r = px * sqrt((i - h/2)^2 + (j - w/2)^2)
+            //         shift = 2 pi f / wl * (1 - sqrt(1 + r^2 / f^2)), stored as uint8
+            const double di = __dsub_rn((double)i, (double)p.H / 2.0);
+            const double dj = __dsub_rn((double)j, (double)p.W / 2.0);
+            const double r = __dmul_rn(p.px, __dsqrt_rn(__dadd_rn(__dmul_rn(di, di), __dmul_rn(dj, dj))));
+            const double q = __ddiv_rn(__dmul_rn(r, r), __dmul_rn(p.focal, p.focal));
+            const double shift = __dmul_rn(p.lens_c, __dsub_rn(1.0, __dsqrt_rn(__dadd_rn(1.0, q))));
+            const uint8_t level = astype_u8(py_mod(shift, kTwoPi));
+            h = py_mod(__dadd_rn(h, (double)level), kTwoPi);
+        }
+        p.out[k] = h;
+    }
 }
 
 struct TrapParams {
@@ -202,6 +248,39 @@ int slm_quantize(const void* src, int src_type, const double* mask, int batch, i
                            static_cast<const int16_t*>(g_in.p), dmask, n, holo, ct2pi, rule, dout);
     FR_TRY(hipGetLastError());
     FR_TRY(hipMemcpyAsync(out, dout, (size_t)n, hipMemcpyDeviceToHost, g_frames_stream));
+    FR_TRY(hipStreamSynchronize(g_frames_stream));
+    return 0;
+}
+
+int slm_transform_hologram(const double* holo_in, int height, int width, int flags, const double* params,
+                           double* holo_out) {
+    if (!holo_out || !params || height < 1 || width < 1) return slm_set_error(SLM_ERR_ARG, "bad arguments");
+    if (flags & ~(SLM_TRANSFORM_DEFLECT | SLM_TRANSFORM_LENS)) return slm_set_error(SLM_ERR_ARG, "unknown flags");
+    if (int rc = slm_current_device_ready()) return rc;
+    std::lock_guard<std::mutex> lk(g_frames_mu);
+    if (!g_frames_stream) FR_TRY(hipStreamCreateWithFlags(&g_frames_stream, hipStreamNonBlocking));
+    const long long n = (long long)height * width;
+    TransformParams p{};
+    if (holo_in) {
+        FR_TRY(g_in.need(sizeof(double) * n));
+        FR_TRY(hipMemcpyAsync(g_in.p, holo_in, sizeof(double) * n, hipMemcpyHostToDevice, g_frames_stream));
+        p.in = static_cast<const double*>(g_in.p);
+    }
+    FR_TRY(g_phase.need(sizeof(double) * n));
+    p.out = static_cast<double*>(g_phase.p);
+    p.H = height;
+    p.W = width;
+    p.deflect = (flags & SLM_TRANSFORM_DEFLECT) != 0;
+    p.lens = (flags & SLM_TRANSFORM_LENS) != 0;
+    p.sin_y = params[0];
+    p.sin_x = params[1];
+    p.ramp_c = params[2];
+    p.lens_c = params[3];
+    p.focal = params[4];
+    p.px = params[5];
+    hipLaunchKernelGGL(transform_kernel, dim3(grid_for(n)), dim3(256), 0, g_frames_stream, p);
+    FR_TRY(hipGetLastError());
+    FR_TRY(hipMemcpyAsync(holo_out, p.out, sizeof(double) * n, hipMemcpyDeviceToHost, g_frames_stream));
     FR_TRY(hipStreamSynchronize(g_frames_stream));
     return 0;
 }

@@ -116,9 +116,28 @@ constexpr int kLdsPair = 80 * 1024;
 #define SLM_ROW_PAIRS 0  // measured equal at 4096 (row quads kept: whole 128-B lines)
 #endif
 
+// Lines per thread. A thread may carry L = 2 rows (row kernels) or columns
+// (column kernels) of the same tile: both lines share the thread's twiddles
+// (cached in registers), its exchange barriers and its address arithmetic, and
+// the two columns of a column tile are one 16-B access. Used for the narrow
+// column plans of SLM_COL_LINES2_MIN_N and longer: one column per thread in
+// 8-wave workgroups could not hold a twiddle cache there (the 4096 column pass
+// had fallen back to table reads inside every pass).
+#ifndef SLM_COL_LINES2_MIN_N
+#define SLM_COL_LINES2_MIN_N 4096  // 4096: col pass 715 -> 626 us for 8 x 4096^2 (twiddles cached again)
+#endif
+#ifndef SLM_ROW_LINES2_MIN_N
+#define SLM_ROW_LINES2_MIN_N 8192  // off: 8 x 4096^2 row pass 695 -> 843 us with row pairs in-thread
+#endif
+template <int K, bool COL>
+constexpr int lines_of() {
+    return (kPlans[K].variant == 1 && PlanOf<K>::N >= (COL ? SLM_COL_LINES2_MIN_N : SLM_ROW_LINES2_MIN_N)) ? 2 : 1;
+}
+
 template <int K>  // plan key of the row length
 struct RowCfg {
     static constexpr int T = PlanOf<K>::T;
+    static constexpr int L = lines_of<K, false>();  // rows per thread
     // rows per workgroup: a row quad (whole 128-B lines of the blocked layout),
     // or a row pair when a quad would not leave room for two workgroups per CU
     // and a pair still fills 8 waves (the partner pair, which reads the other
@@ -127,23 +146,26 @@ struct RowCfg {
     // pairs: twice the workgroups, measured 11.6 -> 9.1 us per 1024^2 row pass.
     static constexpr bool kPairs = (4 * PlanOf<K>::ROWSTRIDE * 8 > kLdsPair && (SLM_ROW_PAIRS || T >= 256)) ||
                                    kPlans[K].variant == 1;
-    // 4096 narrow rows (256 threads per row) run one row per workgroup: two
+    // 4096 narrow rows with one row per thread run one row per workgroup: two
     // workgroups of 4 waves per CU instead of one of 8 (8 x 4096^2 row pass
     // 931 -> 755 us with write-back stores)
-    static constexpr bool kSingle = kPlans[K].variant == 1 && PlanOf<K>::N >= 4096;
+    static constexpr bool kSingle = kPlans[K].variant == 1 && PlanOf<K>::N >= 4096 && L == 1;
 #ifdef SLM_ROW_RPW
     static constexpr int RPW = (T >= 64) ? SLM_ROW_RPW : 256 / T;
 #else
     static constexpr int RPW = (T >= 64) ? (kSingle ? 1 : kPairs ? 2 : 4) : 256 / T;
 #endif
-    static constexpr int QR = RPW < 4 ? RPW : 4;  // rows interleaved across a wave
-    static constexpr int THREADS = RPW * T;
+    static_assert(RPW % L == 0, "rows per workgroup must be a multiple of the rows per thread");
+    static constexpr int RL = RPW / L;              // row groups across lanes
+    static constexpr int QR = RL < 4 ? RL : 4;      // rows interleaved across a wave
+    static constexpr int THREADS = RL * T;
 };
 
 template <int K, int CW>  // plan key of the column length
 struct ColCfg {
     static constexpr int T = PlanOf<K>::T;
-    static constexpr int THREADS = CW * T;
+    static constexpr int L = (CW % 2 == 0) ? lines_of<K, true>() : 1;  // columns per thread
+    static constexpr int THREADS = (CW / L) * T;
     static constexpr bool kValid =
         THREADS >= 64 && THREADS <= 1024 && lds_line(PlanOf<K>::N) * CW * 8 <= 160 * 1024;
 };
@@ -308,7 +330,7 @@ using XchgOf = std::conditional_t<((SLM_F64_XCHG || (kPlans[K].variant == 1 && k
 #ifndef SLM_F64_TWCACHE_MAX
 #define SLM_F64_TWCACHE_MAX 0  // measured neutral at 1024^2 (80 caches the narrow plans)
 #endif
-template <int P, int THREADS, int K, bool COL>
+template <int P, int THREADS, int K, bool COL, int L = 1>
 constexpr int tw_mode() {
     if constexpr (P == 1)
         return TwCountOf<K, RadicesOf<K>>::value * 4 <= SLM_F64_TWCACHE_MAX && THREADS <= 512 ? TW_CACHED
@@ -323,7 +345,11 @@ constexpr int tw_mode() {
     //  * everything else caches every twiddle of the thread. (Row kernels that
     //    form w^2.. from w^1 ran 7-10 % faster at 2048/4096 but took the 4096^2
     //    warm-start parity from 3.1e-6 to 1.3e-5 rms after 100 iterations.)
-    if constexpr (COL && PlanOf<K>::N >= 2048) return TW_DIRECT;
+    //  * two-column threads (L = 2) cache them again: one cache serves both lines
+#ifdef SLM_F32_COL_TW
+    if constexpr (COL) return SLM_F32_COL_TW;
+#endif
+    if constexpr (COL && PlanOf<K>::N >= 2048 && L == 1) return TW_DIRECT;
 #ifdef SLM_F32_ROW_TW
     if constexpr (!COL) return SLM_F32_ROW_TW;
 #endif
@@ -393,9 +419,8 @@ using StateOf = std::conditional_t<std::is_same_v<X, float2>, float2, CplxOf<P>>
 // latency hides behind the transforms and the current tile's stores; the LDS
 // barriers never wait for vector memory (lds_barrier), so the loads stay in
 // flight across them.
-template <bool PERSIST, int NT, class LoadF, class ProcF, class V, int E>
-__device__ __forceinline__ void tile_loop(long long total, LoadF&& load, ProcF&& process, V (&v)[E],
-                                          float (&tv)[NT]) {
+template <bool PERSIST, class LoadF, class ProcF, class VA, class TA>
+__device__ __forceinline__ void tile_loop(long long total, LoadF&& load, ProcF&& process, VA& v, TA& tv) {
     const int G = gridDim.x;
     long long tile = xcd_remap(blockIdx.x, G);
     if (tile >= total) return;
@@ -406,15 +431,13 @@ __device__ __forceinline__ void tile_loop(long long total, LoadF&& load, ProcF&&
         for (;;) {
             const long long next = tile + G;
             const bool more = next < total;
-            V vn[E];
-            float tn[NT];
+            VA vn;
+            TA tn;
             if (more) load(next, vn, tn);
             process(tile, v, tv);
             if (!more) break;
-#pragma unroll
-            for (int m = 0; m < E; ++m) v[m] = vn[m];
-#pragma unroll
-            for (int m = 0; m < NT; ++m) tv[m] = tn[m];
+            __builtin_memcpy(&v, &vn, sizeof(VA));
+            __builtin_memcpy(&tv, &tn, sizeof(TA));
             tile = next;
         }
     }
@@ -437,30 +460,33 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
     constexpr int E = PlanOf<K>::E;
     constexpr int T = PlanOf<K>::T;
     constexpr int RPW = RowCfg<K>::RPW;
+    constexpr int L = RowCfg<K>::L;
     constexpr int LINE = PlanOf<K>::ROWSTRIDE;
     constexpr int TL = T < 16 ? T : 16;
     using X = XchgOf<P, (long long)RPW * LINE, K>;
     using V = StateOf<P, X>;
     __shared__ X smem[RPW * LINE];
 
-    // lane -> (row within the quad, transform thread t): TL consecutive t of
-    // one row, then the next row of the quad. One wave instruction touches
-    // 16 consecutive x of 4 rows = four whole 128-B lines of the blocked layout,
-    // and a 16-lane LDS write group stays inside one row.
+    // lane -> (row group within the quad, transform thread t): TL consecutive
+    // t of one row group, then the next group of the quad. One wave instruction
+    // touches 16 consecutive x of 4 rows = four whole 128-B lines of the
+    // blocked layout, and a 16-lane LDS write group stays inside one row. A
+    // thread carries rows lrow * L + l, l < L.
     constexpr int QR = RowCfg<K>::QR;
     const int tlo = threadIdx.x % TL;
     const int q4 = (threadIdx.x / TL) % QR;
     const int rest = threadIdx.x / (QR * TL);
     const int qq = rest / (T / TL);
     const int t = tlo + TL * (rest - qq * (T / TL));
-    const int lrow = qq * QR + q4;
+    const int lrow = (qq * QR + q4) * L;
     const long long bstep = (long long)T * p.H;  // slot m adds m * bstep (blocked layout)
-    const LdsLine<X> lds{smem + lrow * LINE};
+    const LdsLine<X> lds{smem + lrow * LINE, LINE};
     if constexpr (MODE == ROW_GS_MAIN || MODE == ROW_GD_MAIN) trace_entry(p.trace);
     Twiddles<K, C, tw_mode<P, RowCfg<K>::THREADS, K, false>()> tw;
     load_twiddles<K, C>(tw, t, p.tw);
 
-    // tile = (hologram b, row group g); rows g * RPW + lrow
+    // tile = (hologram b, row group g); rows g * RPW + lrow + l. Row l + 1 of
+    // the blocked layout sits 4 elements after row l.
     auto where = [&](long long tile, int& b, long long& hoff, long long& roff, long long& boff) {
         b = (int)(tile / p.ntile);
         const int row = (int)(tile - (long long)b * p.ntile) * RPW + lrow;
@@ -468,35 +494,39 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
         roff = (long long)row * W;                  // row-major (user arrays)
         boff = hoff + blk_index(row, t, p.H);       // blocked (state)
     };
-    auto load = [&](long long tile, V (&v)[E], float (&)[1]) {
+    auto load = [&](long long tile, V (&v)[L][E], float (&)[1]) {
         int b;
         long long hoff, roff, boff;
         where(tile, b, hoff, roff, boff);
-        auto ain_at = [&](int m) -> S { return p.ain ? (S)p.ain[roff + t + T * m] : (S)1; };
-        if constexpr (MODE == ROW_PHASE_FWD) {
+        auto ain_at = [&](int l, int m) -> S { return p.ain ? (S)p.ain[roff + l * W + t + T * m] : (S)1; };
 #pragma unroll
-            for (int m = 0; m < E; ++m) {
-                S sn, cs;
-                if constexpr (P == 0)
-                    sincosf(p.phase_in[hoff + roff + t + T * m], &sn, &cs);
-                else
-                    sincos((double)p.phase_in[hoff + roff + t + T * m], &sn, &cs);
-                const S a = ain_at(m);
-                v[m] = cv<V>(mk<C>(a * cs, a * sn));
+        for (int l = 0; l < L; ++l) {
+            if constexpr (MODE == ROW_PHASE_FWD) {
+#pragma unroll
+                for (int m = 0; m < E; ++m) {
+                    S sn, cs;
+                    if constexpr (P == 0)
+                        sincosf(p.phase_in[hoff + roff + l * W + t + T * m], &sn, &cs);
+                    else
+                        sincos((double)p.phase_in[hoff + roff + l * W + t + T * m], &sn, &cs);
+                    const S a = ain_at(l, m);
+                    v[l][m] = cv<V>(mk<C>(a * cs, a * sn));
+                }
+            } else if constexpr (MODE == ROW_GD_INIT_FIELD) {
+#pragma unroll
+                for (int m = 0; m < E; ++m)
+                    v[l][m] = cv<V>(normalize(from_c64<C>(p.field[boff + 4 * l + m * bstep]), ain_at(l, m)));
+            } else {
+#pragma unroll
+                for (int m = 0; m < E; ++m) v[l][m] = cv<V>(p.in[boff + 4 * l + m * bstep]);
             }
-        } else if constexpr (MODE == ROW_GD_INIT_FIELD) {
-#pragma unroll
-            for (int m = 0; m < E; ++m) v[m] = cv<V>(normalize(from_c64<C>(p.field[boff + m * bstep]), ain_at(m)));
-        } else {
-#pragma unroll
-            for (int m = 0; m < E; ++m) v[m] = cv<V>(p.in[boff + m * bstep]);
         }
     };
-    auto process = [&](long long tile, V (&v)[E], float (&)[1]) {
+    auto process = [&](long long tile, V (&v)[L][E], float (&)[1]) {
         int b;
         long long hoff, roff, boff;
         where(tile, b, hoff, roff, boff);
-        auto ain_at = [&](int m) -> S { return p.ain ? (S)p.ain[roff + t + T * m] : (S)1; };
+        auto ain_at = [&](int l, int m) -> S { return p.ain ? (S)p.ain[roff + l * W + t + T * m] : (S)1; };
         // timeline of the iteration launches only (SLM_TRACE)
         unsigned long long* const trace = (MODE == ROW_GS_MAIN || MODE == ROW_GD_MAIN) ? p.trace : nullptr;
         trace_point(trace, tile, 0, false);
@@ -507,8 +537,8 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
         }
         trace_point(trace, tile, 1, true);
         if constexpr (MODE == ROW_GS_PHASE) {
-            fft_line_epi<K, true, C>(v, t, tw, lds, [&](int m, C& z) {
-                p.phase_out[hoff + roff + t + T * m] = (float)atan2(z.y, z.x);
+            fft_line_epi<K, true, C>(v, t, tw, lds, [&](int l, int m, C& z) {
+                p.phase_out[hoff + roff + l * W + t + T * m] = (float)atan2(z.y, z.x);
             });
             return;
         } else if constexpr (MODE == ROW_FFT_INV || MODE == ROW_FFT_FWD) {
@@ -517,12 +547,12 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
             fft_line<K, false, C>(v, t, tw, lds);
         } else if constexpr (MODE == ROW_GS_MAIN) {
             // A -> B = a_in A/|A| (src/algorithms.py:30)
-            fft_pair<K, true, false, C>(v, t, tw, lds, [&](int m, C& z) { z = unit_scale(z, ain_at(m)); });
+            fft_pair<K, true, false, C>(v, t, tw, lds, [&](int l, int m, C& z) { z = unit_scale(z, ain_at(l, m)); });
         } else if constexpr (MODE == ROW_GD_INIT_Y) {
-            fft_pair<K, true, false, C>(v, t, tw, lds, [&](int m, C& z) {
-                const S a = ain_at(m);
+            fft_pair<K, true, false, C>(v, t, tw, lds, [&](int l, int m, C& z) {
+                const S a = ain_at(l, m);
                 const C x = unit_scale(z, a);  // a_in exp(i angle(ifft2(sqrt T)))
-                p.field[boff + m * bstep] = to_c64(x);
+                p.field[boff + 4 * l + m * bstep] = to_c64(x);
                 z = normalize(x, a);
             });
         } else if constexpr (MODE == ROW_GD_MAIN) {
@@ -530,10 +560,10 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
             // input -= lr * dEdX (:91); next forward input x/|x| a_in (:84).
             const S lr = (S)p.lr[p.iter];
             const S inv_s = (S)1 / (S)p.holo;
-            fft_pair<K, true, false, C>(v, t, tw, lds, [&](int m, C& z) {
-                const S a = ain_at(m);
+            fft_pair<K, true, false, C>(v, t, tw, lds, [&](int l, int m, C& z) {
+                const S a = ain_at(l, m);
                 const C g = mk<C>(z.x * inv_s * a, z.y * inv_s * a);
-                const long long idx = boff + m * bstep;
+                const long long idx = boff + 4 * l + m * bstep;
                 C x = from_c64<C>(p.field[idx]);
                 const S ax2 = x.x * x.x + x.y * x.y;
                 const S inv = rsqrt_nr(ax2);
@@ -549,11 +579,20 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
             });
         }
         trace_point(trace, tile, 2, false);
+        if (p.wt) {  // uniform: one branch per tile, not per store
 #pragma unroll
-        for (int m = 0; m < E; ++m) store_field(p.out + boff + m * bstep, cv<float2>(v[m]), p.wt);
+            for (int l = 0; l < L; ++l)
+#pragma unroll
+                for (int m = 0; m < E; ++m) store_field(p.out + boff + 4 * l + m * bstep, cv<float2>(v[l][m]), 1);
+        } else {
+#pragma unroll
+            for (int l = 0; l < L; ++l)
+#pragma unroll
+                for (int m = 0; m < E; ++m) p.out[boff + 4 * l + m * bstep] = cv<float2>(v[l][m]);
+        }
         trace_point(trace, tile, 3, true);
     };
-    V v[E];
+    V v[L][E];
     float none[1];
     tile_loop<tile_persistent(P, E)>(p.ntile * (long long)p.B, load, process, v, none);
 }
@@ -574,21 +613,64 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
     constexpr int H = PlanOf<K>::N;
     constexpr int E = PlanOf<K>::E;
     constexpr int T = PlanOf<K>::T;
+    constexpr int L = ColCfg<K, CW>::L;
     constexpr int LINE = PlanOf<K>::LINE;
     constexpr int THREADS = ColCfg<K, CW>::THREADS;
     using X = XchgOf<P, (long long)LINE * CW, K>;
     using V = StateOf<P, X>;
     __shared__ X smem[LINE * CW];
 
-    const int c = threadIdx.x % CW;
-    const int t = threadIdx.x / CW;
+    // a thread carries columns c .. c + L - 1 of the tile (adjacent in the
+    // blocked layout: one 16-B access for L = 2)
+    const int c = (threadIdx.x % (CW / L)) * L;
+    const int t = threadIdx.x / (CW / L);
     constexpr long long kStep = 4LL * T;  // blocked layout: row y = t + T m
     const LdsTile<CW, X> lds{smem, c};
     if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD) trace_entry(p.trace);
-    Twiddles<K, C, tw_mode<P, THREADS, K, true>()> tw;
+    Twiddles<K, C, tw_mode<P, THREADS, K, true, L>()> tw;
     load_twiddles<K, C>(tw, t, p.tw);
     constexpr bool kTarget = (MODE == COL_GS_MAIN || MODE == COL_GD_STATS || MODE == COL_GD_GRAD);
     constexpr int NT = kTarget ? E : 1;
+
+    // field / target element (row t + T m, column c + l) of a tile at base
+    auto ld_field = [&](const float2* src, long long idx, V (&v)[L][E], int m) {
+        if constexpr (L == 2) {
+            const float4 q = *reinterpret_cast<const float4*>(src + idx);
+            v[0][m] = cv<V>(make_float2(q.x, q.y));
+            v[1][m] = cv<V>(make_float2(q.z, q.w));
+        } else {
+            v[0][m] = cv<V>(src[idx]);
+        }
+    };
+    auto ld_tgt = [&](long long idx, float (&tv)[L][NT], int m) {
+        if constexpr (L == 2 && TT == TGT_F32) {
+            const float2 q = *reinterpret_cast<const float2*>(static_cast<const float*>(p.tgt) + idx);
+            tv[0][m] = q.x;
+            tv[1][m] = q.y;
+        } else {
+#pragma unroll
+            for (int l = 0; l < L; ++l) tv[l][m] = TgtLoad<TT>::load(p.tgt, idx + l);
+        }
+    };
+    // stores of a whole tile; `wt` is uniform, so it branches once per tile
+    auto st_tile = [&](long long base, const V (&v)[L][E]) {
+        if (p.wt) {
+#pragma unroll
+            for (int m = 0; m < E; ++m)
+#pragma unroll
+                for (int l = 0; l < L; ++l) store_field(p.out + base + m * kStep + l, cv<float2>(v[l][m]), 1);
+        } else {
+#pragma unroll
+            for (int m = 0; m < E; ++m) {
+                if constexpr (L == 2) {
+                    const float2 a = cv<float2>(v[0][m]), b = cv<float2>(v[1][m]);
+                    *reinterpret_cast<float4*>(p.out + base + m * kStep) = make_float4(a.x, a.y, b.x, b.y);
+                } else {
+                    p.out[base + m * kStep] = cv<float2>(v[0][m]);
+                }
+            }
+        }
+    };
 
     // tile = (hologram b, column panel wg); element (y, x) at blk_index(y, x, H)
     auto where = [&](long long tile, int& b, int& wg, long long& base) {
@@ -596,33 +678,35 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
         wg = (int)(tile - (long long)b * p.nwg);
         base = (long long)b * p.holo + blk_index(t, wg * CW + c, H);
     };
-    auto load = [&](long long tile, V (&v)[E], float (&tv)[NT]) {
+    auto load = [&](long long tile, V (&v)[L][E], float (&tv)[L][NT]) {
         int b, wg;
         long long base;
         where(tile, b, wg, base);
         if constexpr (MODE == COL_REAL_INV) {
 #pragma unroll
-            for (int m = 0; m < E; ++m) {
-                const float a = TgtLoad<TT>::amp(TgtLoad<TT>::load(p.tgt, base + m * kStep));
-                v[m] = cv<V>(mk<C>((S)a, (S)0));
-            }
+            for (int l = 0; l < L; ++l)
+#pragma unroll
+                for (int m = 0; m < E; ++m) {
+                    const float a = TgtLoad<TT>::amp(TgtLoad<TT>::load(p.tgt, base + l + m * kStep));
+                    v[l][m] = cv<V>(mk<C>((S)a, (S)0));
+                }
         } else if constexpr (MODE == COL_EXPECTED) {
             // GD keeps X of iteration i in buffer i % 2; GS passes the same buffer twice.
             const int s = min(p.stop_iter[b], p.loops - 1);
             const float2* src = (s & 1) ? p.in_alt : p.in;
 #pragma unroll
-            for (int m = 0; m < E; ++m) v[m] = cv<V>(src[base + m * kStep]);
+            for (int m = 0; m < E; ++m) ld_field(src, base + m * kStep, v, m);
         } else {
 #pragma unroll
-            for (int m = 0; m < E; ++m) v[m] = cv<V>(p.in[base + m * kStep]);
+            for (int m = 0; m < E; ++m) ld_field(p.in, base + m * kStep, v, m);
         }
         if constexpr (kTarget) {
             // the target is consumed in the middle of the transforms: fetch it with the field
 #pragma unroll
-            for (int m = 0; m < E; ++m) tv[m] = TgtLoad<TT>::load(p.tgt, base + m * kStep);
+            for (int m = 0; m < E; ++m) ld_tgt(base + m * kStep, tv, m);
         }
     };
-    auto process = [&](long long tile, V (&v)[E], float (&tv)[NT]) {
+    auto process = [&](long long tile, V (&v)[L][E], float (&tv)[L][NT]) {
         int b, wg;
         long long base;
         where(tile, b, wg, base);
@@ -648,33 +732,33 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
         trace_point(trace, tile, 1, true);
         if constexpr (MODE == COL_REAL_INV || MODE == COL_FFT_INV || MODE == COL_FFT_FWD) {
             fft_line<K, MODE != COL_FFT_FWD, C>(v, t, tw, lds);
-#pragma unroll
-            for (int m = 0; m < E; ++m) store_field(p.out + base + m * kStep, cv<float2>(v[m]), p.wt);
+            st_tile(base, v);
             return;
         } else if constexpr (MODE == COL_EXPECTED) {
             const long long nat = (long long)b * p.holo + (long long)t * p.W + x;  // row-major output
-            fft_line_epi<K, false, C>(v, t, tw, lds, [&](int m, C& z) {
-                p.e_out[nat + (long long)m * T * p.W] = (float)(z.x * z.x + z.y * z.y);
+            fft_line_epi<K, false, C>(v, t, tw, lds, [&](int l, int m, C& z) {
+                p.e_out[nat + l + (long long)m * T * p.W] = (float)(z.x * z.x + z.y * z.y);
             });
             return;
         } else {
             double mx = 0.0, s2 = 0.0, st = 0.0;
             const S norm = (MODE == COL_GD_GRAD) ? (S)p.norm[b] : (S)0;
-            auto epi = [&](int m, C& z) {
+            auto epi = [&](int l, int m, C& z) {
                 const S e = z.x * z.x + z.y * z.y;
+                const float tl = tv[l][m];
                 if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_STATS) {
                     // |C|^2 as the reference's float64 expected_outcome sees it
                     const double ed = (double)(float)e;
                     mx = fmax(mx, ed);
                     s2 += ed * ed;
-                    st += ed * (double)tv[m];
+                    st += ed * (double)tl;
                 }
                 if constexpr (MODE == COL_GS_MAIN) {
-                    z = unit_scale(z, (S)TgtLoad<TT>::amp(tv[m]));  // D = a_T C/|C| (src/algorithms.py:33)
+                    z = unit_scale(z, (S)TgtLoad<TT>::amp(tl));  // D = a_T C/|C| (src/algorithms.py:33)
                 } else if constexpr (MODE == COL_GD_GRAD) {
                     // mask * F * (output - T), output = |F|^2 norm / max (src/algorithms.py:80,85-88)
                     const S o = e * norm / maxp;
-                    const S w = ((S)1 + (S)p.wa * (S)tv[m] / (S)255) * (o - (S)tv[m]);
+                    const S w = ((S)1 + (S)p.wa * (S)tl / (S)255) * (o - (S)tl);
                     z = mk<C>(z.x * w, z.y * w);
                 }
             };
@@ -693,15 +777,12 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
                 }
             }
             trace_point(trace, tile, 2, false);
-            if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD) {
-#pragma unroll
-                for (int m = 0; m < E; ++m) store_field(p.out + base + m * kStep, cv<float2>(v[m]), p.wt);
-            }
+            if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD) st_tile(base, v);
             trace_point(trace, tile, 3, true);
         }
     };
-    V v[E];
-    float tv[NT];
+    V v[L][E];
+    float tv[L][NT];
     tile_loop<tile_persistent(P, E)>(p.nwg * (long long)p.B, load, process, v, tv);
 }
 

@@ -76,6 +76,15 @@ ColFn SLM_PASTE(col_fn_, SLM_N)(int cw, int mode, int tt, int prec) {
 
 int SLM_PASTE(row_threads_, SLM_N)() { return RowCfg<SLM_N>::THREADS; }
 int SLM_PASTE(row_rpw_, SLM_N)() { return RowCfg<SLM_N>::RPW; }
-int SLM_PASTE(col_threads_, SLM_N)(int cw) { return cw * PlanOf<SLM_N>::T; }
+int SLM_PASTE(col_threads_, SLM_N)(int cw) {
+    switch (cw) {
+        case 1: return ColCfg<SLM_N, 1>::THREADS;
+        case 2: return ColCfg<SLM_N, 2>::THREADS;
+        case 4: return ColCfg<SLM_N, 4>::THREADS;
+        case 8: return ColCfg<SLM_N, 8>::THREADS;
+        case 16: return ColCfg<SLM_N, 16>::THREADS;
+        default: return 0;
+    }
+}
 
 }  // namespace slm

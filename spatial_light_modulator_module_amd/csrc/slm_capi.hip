@@ -887,6 +887,19 @@ int slm_plan_read_target_stats(slm_plan* p, double* norm, double* sum_t2) {
     return 0;
 }
 
+int slm_plan_set_target_stats(slm_plan* p, const double* norm, const double* sum_t2) {
+    if (!p || !norm || !sum_t2) return fail(SLM_ERR_ARG, "null argument");
+    if (!p->target_set) return fail(SLM_ERR_STATE, "target not set");
+    HIP_TRY(hipSetDevice(p->device));
+    std::vector<float> nf(p->B);
+    for (int b = 0; b < p->B; ++b) nf[b] = (float)norm[b];
+    HIP_TRY(hipMemcpyAsync(p->norm, norm, (size_t)p->B * sizeof(double), hipMemcpyHostToDevice, p->stream));
+    HIP_TRY(hipMemcpyAsync(p->normf, nf.data(), (size_t)p->B * sizeof(float), hipMemcpyHostToDevice, p->stream));
+    HIP_TRY(hipMemcpyAsync(p->sum_t2, sum_t2, (size_t)p->B * sizeof(double), hipMemcpyHostToDevice, p->stream));
+    HIP_TRY(hipStreamSynchronize(p->stream));
+    return 0;
+}
+
 long long slm_plan_kernel_bytes(slm_plan* p, int cls) {
     if (!p) return -1;
     const long long px = (long long)p->B * p->holo;
@@ -973,6 +986,41 @@ int slm_fft2(const float* in, float* out, int batch, int height, int width, int 
     }
     free_plan(p);
     return rc;
+}
+
+int slm_fft2_intensity(const float* phase, int batch, int height, int width, float* intensity_out) {
+    if (!phase || !intensity_out) return fail(SLM_ERR_ARG, "null argument");
+    slm_plan* p = nullptr;
+    RC(slm_plan_create(SLM_ALGO_GS, batch, height, width, SLM_TGT_F32, 0, 1, &p));
+    int rc = slm_plan_set_phase(p, phase);
+    if (!rc) {
+        // fft2(exp(1j phase)) = column FFT of the row-transformed field; |.|^2 row-major
+        RowParams rp = row_params(p);
+        rp.out = p->xa;
+        rc = launch(p, SLM_KERNEL_OTHER, fill_int_kernel, dim3((p->B + 255) / 256), dim3(256), p->stop, p->B,
+                    (int)INT_MAX);
+        if (!rc) rc = launch_row(p, ROW_PHASE_FWD, rp, SLM_KERNEL_OTHER);
+        ColParams cp = col_params(p);
+        cp.loops = 1;
+        cp.in = p->xa;
+        cp.in_alt = p->xa;
+        if (!rc) rc = launch_col(p, COL_EXPECTED, cp, SLM_KERNEL_OTHER);
+    }
+    if (!rc) rc = slm_plan_read(p, nullptr, intensity_out, nullptr, nullptr);
+    free_plan(p);
+    return rc;
+}
+
+int slm_plan_read_field(slm_plan* p, float* field) {
+    if (!p || !field) return fail(SLM_ERR_ARG, "null argument");
+    if (p->algo != SLM_ALGO_GD) return fail(SLM_ERR_STATE, "the field is the state of GD plans");
+    HIP_TRY(hipSetDevice(p->device));
+    const long long n = (long long)p->B * p->holo;
+    // p->y is scratch between runs (every run rewrites it before reading it)
+    RC(relayout((const float2*)p->field, p->y, n, p->H, p->W, false, p->stream));
+    HIP_TRY(hipStreamSynchronize(p->stream));
+    HIP_TRY(hipMemcpy(field, p->y, (size_t)n * sizeof(float2), hipMemcpyDeviceToHost));
+    return 0;
 }
 
 int slm_comm_unique_id(unsigned char* id128) {

@@ -6,8 +6,11 @@ output names and .npy format), with the GS / GD loop on the MI355X.
 Target preparation (PIL: grey-scale, invert, pad to square, quarterize,
 resize to the 1024x768 SLM) follows src/generate_hologram.py:45-110; the
 deflect / lens post-processing (:82-87, :178-203, src/wavefront_correction.py:
-440-449) runs vectorised on the host, bit-compatible with the reference's
-per-pixel loops (including lens()'s uint8 truncation).
+440-449) is one element-wise float64 kernel (slm_transform_hologram), bit for
+bit the reference's per-pixel loops (including lens()'s uint8 truncation), and
+the preview's |fft2(exp(1j h))|^2 (:24-34) runs on the plan kernels
+(slm_fft2_intensity). The vectorised NumPy forms below (deflect_2pi, lens)
+remain as the host twins the CPU tests pin against the reference loops.
 """
 from __future__ import annotations
 
@@ -16,6 +19,7 @@ import os
 
 import numpy as np
 
+from . import _lib
 from . import constants as c
 from .algorithms import gerchberg_saxton, gradient_descent
 
@@ -32,14 +36,18 @@ def main(args):
     return save_hologram_and_gif(hologram, args)
 
 
+def expected_outcome_image(hologram, norm):
+    """|fft2(exp(1j h))|^2 / max * norm as float64 (src/generate_hologram.py:25-30);
+    the transform runs on the GPU in complex64 (a preview image)."""
+    intensity = _lib.fft2_intensity(np.asarray(hologram)).astype(np.float64)
+    return intensity / np.amax(intensity) * norm
+
+
 def show_expected_outcome(hologram, args):
-    """src/generate_hologram.py:24-34 (host preview of |fft2(e^{i h})|^2)."""
+    """src/generate_hologram.py:24-34."""
     from PIL import Image
 
-    expected_outcome = np.fft.fft2(np.exp(1j * hologram))
-    norm = find_out_norm(args)
-    intensity = np.abs(expected_outcome) ** 2
-    normed = intensity / np.amax(intensity) * norm
+    normed = expected_outcome_image(hologram, find_out_norm(args))
     Image.fromarray(normed).resize((c.slm_height, c.slm_height)).show()
 
 
@@ -100,12 +108,32 @@ def make_hologram(args):
     return hologram
 
 
+def deflect_params(angle):
+    """The host-side scalars of deflect_2pi (src/wavefront_correction.py:440-447),
+    computed exactly as the reference computes them."""
+    x_angle, y_angle = angle
+    const = 2 * np.pi * c.px_distance / c.wavelength
+    return float(np.sin(y_angle * c.u)), float(np.sin(x_angle * c.u)), const
+
+
+def lens_params(focal_length):
+    """The host-side scalars of lens() (src/generate_hologram.py:189-203)."""
+    return 2 * np.pi * focal_length / c.wavelength, float(focal_length), c.px_distance
+
+
 def transform_hologram(hologram, args):
-    if args.deflect is not None:
-        hologram = deflect_hologram(hologram, args.deflect)
-    if args.lens:
-        hologram = add_lens(hologram, args.lens)
-    return hologram
+    """src/generate_hologram.py:82-87 as one GPU launch (slm_transform_hologram).
+    The reference's deflect ramp has the SLM's size (c.slm_height x c.slm_width),
+    so the hologram must have it too when deflecting (as in the reference)."""
+    d = deflect_params(args.deflect) if args.deflect is not None else None
+    f = lens_params(args.lens) if args.lens else None
+    if d is None and f is None:
+        return hologram
+    h, w = np.asarray(hologram).shape
+    if d is not None and (h, w) != (c.slm_height, c.slm_width):
+        raise ValueError(f"operands could not be broadcast together with shapes {(h, w)} "
+                         f"{(c.slm_height, c.slm_width)}")
+    return _lib.transform_hologram(hologram, h, w, d, f)
 
 
 def add_gif_dirs(args):

@@ -74,16 +74,13 @@ def test_lens_is_bitwise_the_reference_loop(f):
     np.testing.assert_array_equal(gh.lens(f, (48, 64)), _lens_loop(f, (48, 64)))
 
 
-def test_analytical_hologram_cli(tmp_path, monkeypatch):
-    monkeypatch.chdir(tmp_path)
-    path = gh.cli(["-deflect", "1", "0.5", "-lens", "2.0", "-dest_dir", "out"])
-    assert os.path.basename(path) == "analytical_deflect_x1.0_y0.5_lens2.0.npy"
-    h = np.load(path)
-    want = gh.add_lens(gh.deflect_hologram(np.zeros((c.slm_height, c.slm_width)), (1.0, 0.5)), 2.0)
-    np.testing.assert_array_equal(h, want)
-    # a second run does not overwrite: originalize_name appends _1
-    path2 = gh.cli(["-deflect", "1", "0.5", "-lens", "2.0", "-dest_dir", "out"])
-    assert path2.endswith("analytical_deflect_x1.0_y0.5_lens2.0_1.npy")
+def test_transform_scalars_are_the_reference_host_values():
+    """The scalars handed to slm_transform_hologram are the ones the reference's
+    loops compute (src/wavefront_correction.py:443-447, src/generate_hologram.py:194-200)."""
+    sy, sx, k = gh.deflect_params((1.0, 0.5))
+    assert sy == np.sin(0.5 * c.u) and sx == np.sin(1.0 * c.u) and k == 2 * np.pi * c.px_distance / c.wavelength
+    a, f, px = gh.lens_params(2.0)
+    assert a == 2 * np.pi * 2.0 / c.wavelength and f == 2.0 and px == c.px_distance
 
 
 def test_prepare_target_shape_and_padding(tmp_path, monkeypatch):

@@ -17,7 +17,7 @@ for f in $base/kernels_*.o; do
 done
 pids=""
 for k in "$@"; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=fast -fno-slp-vectorize -Wno-unused-function $extra -DSLM_N=$k -c $src/kernels_inst.hip -o $out/kernels_$k.o &
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=${CONTRACT:-fast} -fno-slp-vectorize -Wno-unused-function $extra -DSLM_N=$k -c $src/kernels_inst.hip -o $out/kernels_$k.o &
   pids="$pids $!"
 done
 # the host runtime sees the same macros (grid sizing follows tile_persistent)
