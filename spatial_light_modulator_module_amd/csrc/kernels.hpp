@@ -39,6 +39,7 @@ struct RowParams {
     float2* field;           // GD state x [B][H][W]
     const float* lr;         // GD learning rate per iteration
     const int* stop_iter;    // [B], INT_MAX while running
+    int checked;             // tolerance run: honour stop_iter (else it is never read)
     int iter;                // iteration index of this launch
     int wt;                  // write-through field stores (store_field)
     int W;                   // row length (== template W; kept for checks)
@@ -59,6 +60,7 @@ struct ColParams {
     double* partials;        // [B][max_loops][nwg] x 4 doubles: max, sum E^2, sum E T, 0
     float* e_out;            // |C|^2 of the final iteration [B][H][W]
     const int* stop_iter;    // [B]
+    int checked;             // tolerance run: honour stop_iter (else it is never read)
     const float* norm;       // max(T) per hologram
     int iter;                // iteration index of this launch
     int max_loops;           // partial-slab stride
@@ -359,19 +361,34 @@ constexpr int tw_mode() {
 
 template <int TT>
 struct TgtLoad;
+// Target amplitudes. uint8: numpy's sqrt(uint8) is float16 (SURVEY.md
+// appendix); every sqrt of 0..255 lies >= 100 float32 ulps from a float16
+// rounding midpoint, so the hardware square root (<= 1 ulp) rounds to the same
+// float16. float32: the hardware reciprocal square root plus one Newton
+// (Markstein) correction -- 0 mismatches against the correctly rounded sqrtf
+// over 2e5 random targets, a third of the instructions of the IEEE expansion;
+// zero, denormal, infinite and negative inputs take the hardware sqrt.
 template <>
 struct TgtLoad<TGT_U8> {
     __device__ __forceinline__ static float load(const void* p, long long i) {
         return (float)static_cast<const uint8_t*>(p)[i];
     }
-    __device__ __forceinline__ static float amp(float t) { return __half2float(__float2half_rn(sqrtf(t))); }
+    __device__ __forceinline__ static float amp(float t) {
+        return __half2float(__float2half_rn(__builtin_amdgcn_sqrtf(t)));
+    }
 };
 template <>
 struct TgtLoad<TGT_F32> {
     __device__ __forceinline__ static float load(const void* p, long long i) {
         return static_cast<const float*>(p)[i];
     }
-    __device__ __forceinline__ static float amp(float t) { return sqrtf(t); }
+    __device__ __forceinline__ static float amp(float t) {
+        const float y = __builtin_amdgcn_rsqf(t);
+        const float s = t * y;
+        const float r = fmaf(-s, s, t);
+        const float c = fmaf(r, 0.5f * y, s);
+        return (t >= 1.17549435e-38f && t <= 3.40282347e38f) ? c : __builtin_amdgcn_sqrtf(t);
+    }
 };
 
 // Block-wide reduction of (max, sum, sum); result valid in thread 0.
@@ -530,10 +547,11 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
         // timeline of the iteration launches only (SLM_TRACE)
         unsigned long long* const trace = (MODE == ROW_GS_MAIN || MODE == ROW_GD_MAIN) ? p.trace : nullptr;
         trace_point(trace, tile, 0, false);
+        // (unchecked runs never stop early: no dependent load of the flag)
         if constexpr (MODE == ROW_GS_MAIN) {
-            if (p.iter >= p.stop_iter[b]) return;  // stopped after this iteration's column pass
+            if (p.checked && p.iter >= p.stop_iter[b]) return;  // stopped after this iteration's column pass
         } else if constexpr (MODE == ROW_GD_MAIN) {
-            if (p.iter > p.stop_iter[b]) return;
+            if (p.checked && p.iter > p.stop_iter[b]) return;
         }
         trace_point(trace, tile, 1, true);
         if constexpr (MODE == ROW_GS_PHASE) {
@@ -692,7 +710,7 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
                 }
         } else if constexpr (MODE == COL_EXPECTED) {
             // GD keeps X of iteration i in buffer i % 2; GS passes the same buffer twice.
-            const int s = min(p.stop_iter[b], p.loops - 1);
+            const int s = p.checked ? min(p.stop_iter[b], p.loops - 1) : p.loops - 1;
             const float2* src = (s & 1) ? p.in_alt : p.in;
 #pragma unroll
             for (int m = 0; m < E; ++m) ld_field(src, base + m * kStep, v, m);
@@ -714,7 +732,7 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
         unsigned long long* const trace = (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD) ? p.trace : nullptr;
         trace_point(trace, tile, 0, false);
         if constexpr (kTarget) {
-            if (p.iter > p.stop_iter[b]) return;
+            if (p.checked && p.iter > p.stop_iter[b]) return;
         }
         // GD gradient needs this iteration's global max of |F|^2 (src/algorithms.py:86).
         S maxp = 0;

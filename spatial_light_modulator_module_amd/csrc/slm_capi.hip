@@ -457,6 +457,7 @@ int enqueue_gs(slm_plan* p, int loops, double tol, int checked) {
     RowParams rp = row_params(p);
     ColParams cp = col_params(p);
     cp.loops = loops;
+    rp.checked = cp.checked = checked;
     // setup: X0 = rowFFT(a_in A0/|A0|), A0 = ifft2(sqrt T) (src/algorithms.py:14-27),
     // or the warm start B = a_in exp(i phi).
     if (p->phase_set) {
@@ -496,6 +497,7 @@ int enqueue_gd(slm_plan* p, int loops, double tol, int checked, float wa) {
     RowParams rp = row_params(p);
     ColParams cp = col_params(p);
     cp.loops = loops;
+    rp.checked = cp.checked = checked;
     cp.wa = wa;
     // setup (make_initial_guess, src/algorithms.py:115-158): host-provided field
     // or the "fourier" guess a_in exp(i angle(ifft2(sqrt T))).
