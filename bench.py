@@ -79,16 +79,19 @@ def targets(first: int, count: int, n: int) -> np.ndarray:
 def model_bytes(plan, cls):
     """SURVEY.md 8d algorithmic bytes per launch (unfused-pass byte model):
     GS 68 B/px/iteration = column passes 32 + target 4 (col_main) + row passes
-    32 (row_main); GD 76 = column passes 32 + target 4 (col_main) + row passes
-    16 + gradient epilogue 24 (row_main); the GD statistics pass re-reads X and
-    is not in the model (0). A uint8 target counts 1 B, a_in adds 4 B."""
+    32 (row_main); GD 76 = forward column pass 16 (gd_stats) + inverse column
+    pass with the target 20 (col_main) + row passes 16 + gradient epilogue 24
+    (row_main). A uint8 target counts 1 B, a_in adds 4 B."""
     px = plan.batch * plan.height * plan.width
     tb = 1 if plan.tgt_type == _lib.TGT_U8 else 4
     ab = 4 if plan.has_ain else 0
+    gd = plan.algo == _lib.ALGO_GD
     if cls == _lib.KERNEL_COL_MAIN:
-        return px * (32 + tb)
+        return px * ((16 if gd else 32) + tb)
     if cls == _lib.KERNEL_ROW_MAIN:
-        return px * (32 + ab + (8 if plan.algo == _lib.ALGO_GD else 0))
+        return px * (32 + ab + (8 if gd else 0))
+    if cls == _lib.KERNEL_GD_STATS:
+        return px * 16
     return 0
 
 

@@ -242,9 +242,24 @@ constexpr int occupancy_wpe(int threads, long long lds_bytes) {
 // (column pass), and rows y..y+3 (y % 4 == 0) of a block form one 128-B line
 // (row pass on row quads), so both passes move whole lines. User-facing
 // arrays (phases, a_in, expected output) stay row-major.
+// Two blocked layouts, one per direction of the transpose. X (the row pass's
+// output, the column pass's input, and the target) and Y (the column pass's
+// output, the row pass's input, and the GD field) are [x / P][y][x % P] with
+// their own panel widths P: a column tile reads / writes whole panels of the
+// narrower layout, a row tile whole chunks of the wider one.
+#ifndef SLM_PANEL_X_LOG2
+#define SLM_PANEL_X_LOG2 2
+#endif
+#ifndef SLM_PANEL_Y_LOG2
+#define SLM_PANEL_Y_LOG2 2
+#endif
+enum Layout : int { LAYOUT_X = SLM_PANEL_X_LOG2, LAYOUT_Y = SLM_PANEL_Y_LOG2 };
+template <int PLOG>
 __host__ __device__ __forceinline__ long long blk_index(long long y, int x, int H) {
-    return (((long long)(x >> 2) * H + y) << 2) + (x & 3);
+    return (((long long)(x >> PLOG) * H + y) << PLOG) + (x & ((1 << PLOG) - 1));
 }
+template <int PLOG>
+constexpr int kPanelOf = 1 << PLOG;  // row y + 1 sits kPanelOf elements after row y
 
 // ------------------------------------------------------------------------
 // element-wise pieces
@@ -502,19 +517,22 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
     Twiddles<K, C, tw_mode<P, RowCfg<K>::THREADS, K, false>()> tw;
     load_twiddles<K, C>(tw, t, p.tw);
 
-    // tile = (hologram b, row group g); rows g * RPW + lrow + l. Row l + 1 of
-    // the blocked layout sits 4 elements after row l.
-    auto where = [&](long long tile, int& b, long long& hoff, long long& roff, long long& boff) {
+    // tile = (hologram b, row group g); rows g * RPW + lrow + l. Inputs (Y,
+    // the GD field) are in layout Y, outputs (X) in layout X; row l + 1 sits
+    // kPanelOf<layout> elements after row l.
+    constexpr int PY = kPanelOf<LAYOUT_Y>, PX = kPanelOf<LAYOUT_X>;
+    auto where = [&](long long tile, int& b, long long& hoff, long long& roff, long long& boff, long long& xoff) {
         b = (int)(tile / p.ntile);
         const int row = (int)(tile - (long long)b * p.ntile) * RPW + lrow;
         hoff = (long long)b * p.holo;
-        roff = (long long)row * W;                  // row-major (user arrays)
-        boff = hoff + blk_index(row, t, p.H);       // blocked (state)
+        roff = (long long)row * W;                             // row-major (user arrays)
+        boff = hoff + blk_index<LAYOUT_Y>(row, t, p.H);        // blocked input / field
+        xoff = hoff + blk_index<LAYOUT_X>(row, t, p.H);        // blocked output
     };
     auto load = [&](long long tile, V (&v)[L][E], float (&)[1]) {
         int b;
-        long long hoff, roff, boff;
-        where(tile, b, hoff, roff, boff);
+        long long hoff, roff, boff, xoff;
+        where(tile, b, hoff, roff, boff, xoff);
         auto ain_at = [&](int l, int m) -> S { return p.ain ? (S)p.ain[roff + l * W + t + T * m] : (S)1; };
 #pragma unroll
         for (int l = 0; l < L; ++l) {
@@ -532,17 +550,17 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
             } else if constexpr (MODE == ROW_GD_INIT_FIELD) {
 #pragma unroll
                 for (int m = 0; m < E; ++m)
-                    v[l][m] = cv<V>(normalize(from_c64<C>(p.field[boff + 4 * l + m * bstep]), ain_at(l, m)));
+                    v[l][m] = cv<V>(normalize(from_c64<C>(p.field[boff + PY * l + m * bstep]), ain_at(l, m)));
             } else {
 #pragma unroll
-                for (int m = 0; m < E; ++m) v[l][m] = cv<V>(p.in[boff + 4 * l + m * bstep]);
+                for (int m = 0; m < E; ++m) v[l][m] = cv<V>(p.in[boff + PY * l + m * bstep]);
             }
         }
     };
     auto process = [&](long long tile, V (&v)[L][E], float (&)[1]) {
         int b;
-        long long hoff, roff, boff;
-        where(tile, b, hoff, roff, boff);
+        long long hoff, roff, boff, xoff;
+        where(tile, b, hoff, roff, boff, xoff);
         auto ain_at = [&](int l, int m) -> S { return p.ain ? (S)p.ain[roff + l * W + t + T * m] : (S)1; };
         // timeline of the iteration launches only (SLM_TRACE)
         unsigned long long* const trace = (MODE == ROW_GS_MAIN || MODE == ROW_GD_MAIN) ? p.trace : nullptr;
@@ -570,7 +588,7 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
             fft_pair<K, true, false, C>(v, t, tw, lds, [&](int l, int m, C& z) {
                 const S a = ain_at(l, m);
                 const C x = unit_scale(z, a);  // a_in exp(i angle(ifft2(sqrt T)))
-                p.field[boff + 4 * l + m * bstep] = to_c64(x);
+                p.field[boff + PY * l + m * bstep] = to_c64(x);
                 z = normalize(x, a);
             });
         } else if constexpr (MODE == ROW_GD_MAIN) {
@@ -581,7 +599,7 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
             fft_pair<K, true, false, C>(v, t, tw, lds, [&](int l, int m, C& z) {
                 const S a = ain_at(l, m);
                 const C g = mk<C>(z.x * inv_s * a, z.y * inv_s * a);
-                const long long idx = boff + 4 * l + m * bstep;
+                const long long idx = boff + PY * l + m * bstep;
                 C x = from_c64<C>(p.field[idx]);
                 const S ax2 = x.x * x.x + x.y * x.y;
                 const S inv = rsqrt_nr(ax2);
@@ -601,12 +619,12 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
 #pragma unroll
             for (int l = 0; l < L; ++l)
 #pragma unroll
-                for (int m = 0; m < E; ++m) store_field(p.out + boff + 4 * l + m * bstep, cv<float2>(v[l][m]), 1);
+                for (int m = 0; m < E; ++m) store_field(p.out + xoff + PX * l + m * bstep, cv<float2>(v[l][m]), 1);
         } else {
 #pragma unroll
             for (int l = 0; l < L; ++l)
 #pragma unroll
-                for (int m = 0; m < E; ++m) p.out[boff + 4 * l + m * bstep] = cv<float2>(v[l][m]);
+                for (int m = 0; m < E; ++m) p.out[xoff + PX * l + m * bstep] = cv<float2>(v[l][m]);
         }
         trace_point(trace, tile, 3, true);
     };
@@ -642,7 +660,9 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
     // blocked layout: one 16-B access for L = 2)
     const int c = (threadIdx.x % (CW / L)) * L;
     const int t = threadIdx.x / (CW / L);
-    constexpr long long kStep = 4LL * T;  // blocked layout: row y = t + T m
+    // inputs (X, target) in layout X, outputs (Y) in layout Y: row y = t + T m
+    constexpr long long kStep = (long long)kPanelOf<LAYOUT_X> * T;
+    constexpr long long kStepY = (long long)kPanelOf<LAYOUT_Y> * T;
     const LdsTile<CW, X> lds{smem, c};
     if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD) trace_entry(p.trace);
     Twiddles<K, C, tw_mode<P, THREADS, K, true, L>()> tw;
@@ -670,31 +690,34 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
             for (int l = 0; l < L; ++l) tv[l][m] = TgtLoad<TT>::load(p.tgt, idx + l);
         }
     };
-    // stores of a whole tile; `wt` is uniform, so it branches once per tile
+    // stores of a whole tile (layout Y); `wt` is uniform, so it branches once per tile
     auto st_tile = [&](long long base, const V (&v)[L][E]) {
         if (p.wt) {
 #pragma unroll
             for (int m = 0; m < E; ++m)
 #pragma unroll
-                for (int l = 0; l < L; ++l) store_field(p.out + base + m * kStep + l, cv<float2>(v[l][m]), 1);
+                for (int l = 0; l < L; ++l) store_field(p.out + base + m * kStepY + l, cv<float2>(v[l][m]), 1);
         } else {
 #pragma unroll
             for (int m = 0; m < E; ++m) {
                 if constexpr (L == 2) {
                     const float2 a = cv<float2>(v[0][m]), b = cv<float2>(v[1][m]);
-                    *reinterpret_cast<float4*>(p.out + base + m * kStep) = make_float4(a.x, a.y, b.x, b.y);
+                    *reinterpret_cast<float4*>(p.out + base + m * kStepY) = make_float4(a.x, a.y, b.x, b.y);
                 } else {
-                    p.out[base + m * kStep] = cv<float2>(v[0][m]);
+                    p.out[base + m * kStepY] = cv<float2>(v[0][m]);
                 }
             }
         }
     };
 
-    // tile = (hologram b, column panel wg); element (y, x) at blk_index(y, x, H)
+    // tile = (hologram b, column group wg); element (y, x) at blk_index<layout>(y, x, H)
     auto where = [&](long long tile, int& b, int& wg, long long& base) {
         b = (int)(tile / p.nwg);
         wg = (int)(tile - (long long)b * p.nwg);
-        base = (long long)b * p.holo + blk_index(t, wg * CW + c, H);
+        base = (long long)b * p.holo + blk_index<LAYOUT_X>(t, wg * CW + c, H);
+    };
+    auto out_base = [&](int b, int wg) {
+        return (long long)b * p.holo + blk_index<LAYOUT_Y>(t, wg * CW + c, H);
     };
     auto load = [&](long long tile, V (&v)[L][E], float (&tv)[L][NT]) {
         int b, wg;
@@ -750,7 +773,7 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
         trace_point(trace, tile, 1, true);
         if constexpr (MODE == COL_REAL_INV || MODE == COL_FFT_INV || MODE == COL_FFT_FWD) {
             fft_line<K, MODE != COL_FFT_FWD, C>(v, t, tw, lds);
-            st_tile(base, v);
+            st_tile(out_base(b, wg), v);
             return;
         } else if constexpr (MODE == COL_EXPECTED) {
             const long long nat = (long long)b * p.holo + (long long)t * p.W + x;  // row-major output
@@ -780,6 +803,10 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
                     z = mk<C>(z.x * w, z.y * w);
                 }
             };
+            // GD recomputes F in the gradient pass: storing F from the statistics
+            // pass and reading it back measured slower at 1024^2 (8.9 + 9.5 us
+            // against 5.7 + 10.9 us per iteration: the extra store tail costs
+            // more than the forward transform saves)
             if constexpr (MODE == COL_GD_STATS)
                 fft_line_epi<K, false, C>(v, t, tw, lds, epi);
             else
@@ -795,7 +822,7 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
                 }
             }
             trace_point(trace, tile, 2, false);
-            if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD) st_tile(base, v);
+            if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD) st_tile(out_base(b, wg), v);
             trace_point(trace, tile, 3, true);
         }
     };
@@ -874,19 +901,19 @@ __global__ void __launch_bounds__(256) field_phase_kernel(const float2* field, f
     for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
         const long long b = i / holo, r = i - b * holo;
         const int y = (int)(r / W), x = (int)(r - (long long)y * W);
-        const float2 f = field[b * holo + blk_index(y, x, H)];
+        const float2 f = field[b * holo + blk_index<LAYOUT_Y>(y, x, H)];
         phase[i] = atan2f(f.y, f.x);
     }
 }
 
 // row-major <-> blocked layout (uploads, the FFT test entry)
-template <typename V, bool TO_BLOCKED>
+template <typename V, bool TO_BLOCKED, int PLOG>
 __global__ void __launch_bounds__(256) relayout_kernel(const V* in, V* out, long long n, int H, int W) {
     const long long holo = (long long)H * W;
     for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
         const long long b = i / holo, r = i - b * holo;
         const int y = (int)(r / W), x = (int)(r - (long long)y * W);
-        const long long j = b * holo + blk_index(y, x, H);
+        const long long j = b * holo + blk_index<PLOG>(y, x, H);
         if (TO_BLOCKED)
             out[j] = in[i];
         else

@@ -163,13 +163,14 @@ __global__ void __launch_bounds__(64) target_stats_final_kernel(const double* pa
     }
 }
 
-template <typename V>
+// layout: LAYOUT_X (X buffers, the target) or LAYOUT_Y (Y, the GD field)
+template <int LAYOUT, typename V>
 int relayout(const V* in, V* out, long long n, int H, int W, bool to_blocked, hipStream_t st) {
     const int grid = (int)std::min<long long>(8192, (n + 255) / 256);
     if (to_blocked)
-        hipLaunchKernelGGL((relayout_kernel<V, true>), dim3(grid), dim3(256), 0, st, in, out, n, H, W);
+        hipLaunchKernelGGL((relayout_kernel<V, true, LAYOUT>), dim3(grid), dim3(256), 0, st, in, out, n, H, W);
     else
-        hipLaunchKernelGGL((relayout_kernel<V, false>), dim3(grid), dim3(256), 0, st, in, out, n, H, W);
+        hipLaunchKernelGGL((relayout_kernel<V, false, LAYOUT>), dim3(grid), dim3(256), 0, st, in, out, n, H, W);
     HIP_TRY(hipGetLastError());
     return 0;
 }
@@ -715,11 +716,11 @@ int slm_plan_set_target(slm_plan* p, const void* tgt) {
     if (p->tt == SLM_TGT_U8) {
         hipLaunchKernelGGL(target_stats_partial_kernel<uint8_t>, dim3(kTsBlocks, p->B), dim3(256), 0, p->stream,
                            (const uint8_t*)stage, p->holo, p->ts_part);
-        RC(relayout((const uint8_t*)stage, (uint8_t*)p->tgt, n, p->H, p->W, true, p->stream));
+        RC(relayout<LAYOUT_X>((const uint8_t*)stage, (uint8_t*)p->tgt, n, p->H, p->W, true, p->stream));
     } else {
         hipLaunchKernelGGL(target_stats_partial_kernel<float>, dim3(kTsBlocks, p->B), dim3(256), 0, p->stream,
                            (const float*)stage, p->holo, p->ts_part);
-        RC(relayout((const float*)stage, (float*)p->tgt, n, p->H, p->W, true, p->stream));
+        RC(relayout<LAYOUT_X>((const float*)stage, (float*)p->tgt, n, p->H, p->W, true, p->stream));
     }
     hipLaunchKernelGGL(target_stats_final_kernel, dim3(p->B), dim3(kTsBlocks), 0, p->stream, p->ts_part, p->norm,
                        p->normf, p->sum_t2);
@@ -778,7 +779,7 @@ int slm_plan_set_field(slm_plan* p, const float* field) {
     }
     const long long n = (long long)p->B * p->holo;
     HIP_TRY(hipMemcpyAsync(p->y, field, (size_t)n * sizeof(float2), hipMemcpyHostToDevice, p->stream));
-    RC(relayout((const float2*)p->y, p->field, n, p->H, p->W, true, p->stream));
+    RC(relayout<LAYOUT_Y>((const float2*)p->y, p->field, n, p->H, p->W, true, p->stream));
     HIP_TRY(hipStreamSynchronize(p->stream));
     p->field_set = true;
     return 0;
@@ -908,7 +909,7 @@ long long slm_plan_kernel_bytes(slm_plan* p, int cls) {
     const long long tb = p->tt == SLM_TGT_U8 ? 1 : 4;
     const long long ab = p->has_ain ? 4 : 0;
     switch (cls) {
-        case SLM_KERNEL_COL_MAIN: return px * (8 + tb + 8);       // X in, T in, Y out
+        case SLM_KERNEL_COL_MAIN: return px * (8 + tb + 8);       // X (GD: F) in, T in, Y out
         case SLM_KERNEL_ROW_MAIN:                                 // Y in, X out (+ a_in) (+ field r/w for GD)
             return px * (16 + ab + (p->algo == SLM_ALGO_GD ? 16 : 0));
         case SLM_KERNEL_GD_STATS: return px * (8 + tb);           // X in, T in
@@ -967,7 +968,7 @@ int slm_fft2(const float* in, float* out, int batch, int height, int width, int 
     int rc = 0;
     hipError_t e = hipMemcpyAsync(p->y, in, bytes, hipMemcpyHostToDevice, p->stream);
     if (e != hipSuccess) rc = fail(SLM_ERR_HIP, "upload failed: %s", hipGetErrorString(e));
-    if (!rc) rc = relayout((const float2*)p->y, p->xa, n, height, width, true, p->stream);
+    if (!rc) rc = relayout<LAYOUT_Y>((const float2*)p->y, p->xa, n, height, width, true, p->stream);  // row-pass input
     if (!rc) {
         RowParams rp = row_params(p);
         rp.in = p->xa;
@@ -980,7 +981,7 @@ int slm_fft2(const float* in, float* out, int batch, int height, int width, int 
         cp.out = p->xa;
         rc = launch_col(p, inverse ? COL_FFT_INV : COL_FFT_FWD, cp, SLM_KERNEL_OTHER);
     }
-    if (!rc) rc = relayout((const float2*)p->xa, p->y, n, height, width, false, p->stream);
+    if (!rc) rc = relayout<LAYOUT_Y>((const float2*)p->xa, p->y, n, height, width, false, p->stream);  // col-pass output
     if (!rc) {
         e = hipStreamSynchronize(p->stream);
         if (e == hipSuccess) e = hipMemcpy(out, p->y, bytes, hipMemcpyDeviceToHost);
@@ -1019,7 +1020,7 @@ int slm_plan_read_field(slm_plan* p, float* field) {
     HIP_TRY(hipSetDevice(p->device));
     const long long n = (long long)p->B * p->holo;
     // p->y is scratch between runs (every run rewrites it before reading it)
-    RC(relayout((const float2*)p->field, p->y, n, p->H, p->W, false, p->stream));
+    RC(relayout<LAYOUT_Y>((const float2*)p->field, p->y, n, p->H, p->W, false, p->stream));
     HIP_TRY(hipStreamSynchronize(p->stream));
     HIP_TRY(hipMemcpy(field, p->y, (size_t)n * sizeof(float2), hipMemcpyDeviceToHost));
     return 0;
