@@ -439,6 +439,18 @@ __device__ __forceinline__ void block_reduce_stats(double& mx, double& s2, doubl
 template <int P, class X>
 using StateOf = std::conditional_t<std::is_same_v<X, float2>, float2, CplxOf<P>>;
 
+// Kernel-argument prologue: the fields a tile's addresses need, pulled into
+// SGPRs together (one scalar round trip; left to itself the compiler issues one
+// per branch of the tile setup before the first field load can go out).
+template <class A>
+__device__ __forceinline__ void sgpr_pin1(const A& a) {
+    asm volatile("" ::"s"(a));
+}
+template <class... A>
+__device__ __forceinline__ void sgpr_pin(const A&... a) {
+    (sgpr_pin1(a), ...);
+}
+
 // ------------------------------------------------------------------------
 // persistent tile loop (both passes)
 // ------------------------------------------------------------------------
@@ -514,6 +526,7 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
     const long long bstep = (long long)T * p.H;  // slot m adds m * bstep (blocked layout)
     const LdsLine<X> lds{smem + lrow * LINE, LINE};
     if constexpr (MODE == ROW_GS_MAIN || MODE == ROW_GD_MAIN) trace_entry(p.trace);
+    sgpr_pin(p.in, p.out, p.holo, p.H, p.B, p.ntile, p.tw, p.ain, p.wt, gridDim.x);
     Twiddles<K, C, tw_mode<P, RowCfg<K>::THREADS, K, false>()> tw;
     load_twiddles<K, C>(tw, t, p.tw);
 
@@ -665,6 +678,7 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
     constexpr long long kStepY = (long long)kPanelOf<LAYOUT_Y> * T;
     const LdsTile<CW, X> lds{smem, c};
     if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD) trace_entry(p.trace);
+    sgpr_pin(p.in, p.out, p.tgt, p.holo, p.nwg, p.B, p.tw, p.checked, p.wt, gridDim.x);
     Twiddles<K, C, tw_mode<P, THREADS, K, true, L>()> tw;
     load_twiddles<K, C>(tw, t, p.tw);
     constexpr bool kTarget = (MODE == COL_GS_MAIN || MODE == COL_GD_STATS || MODE == COL_GD_GRAD);
@@ -811,6 +825,9 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
                 fft_line_epi<K, false, C>(v, t, tw, lds, epi);
             else
                 fft_pair<K, false, true, C>(v, t, tw, lds, epi);
+            trace_point(trace, tile, 2, false);
+            if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD) st_tile(out_base(b, wg), v);
+            // the cross-lane statistics reduction (LDS only) runs while the field stores drain
             if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_STATS) {
                 block_reduce_stats<THREADS>(mx, s2, st);
                 if (threadIdx.x == 0) {
@@ -821,8 +838,6 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
                     dst[3] = 0.0;
                 }
             }
-            trace_point(trace, tile, 2, false);
-            if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD) st_tile(out_base(b, wg), v);
             trace_point(trace, tile, 3, true);
         }
     };
