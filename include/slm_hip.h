@@ -113,6 +113,9 @@ long long slm_plan_kernel_bytes(slm_plan* plan, int kernel_class);
  * info[5] / info[6] = radix plan keys of rows / columns, info[7] = precision
  * (info must hold 8 ints) */
 int slm_plan_info(slm_plan* plan, int* info);
+/* panel widths (log2) of the plan's two blocked device layouts: X (row-pass
+ * output, column-pass input, target) and Y (column-pass output, GD field) */
+int slm_plan_layout(slm_plan* plan, int* x_log2, int* y_log2);
 
 /* Diagnostics: per-workgroup phase timestamps (s_memrealtime, 100 MHz: tile
  * start, loads complete, transforms done, stores complete, kernel entry) plus

@@ -71,6 +71,7 @@ _SIGNATURES = [
     ("slm_plan_read_field", _c_int, [_vp, _vp]),
     ("slm_plan_kernel_bytes", ctypes.c_longlong, [_vp, _c_int]),
     ("slm_plan_info", _c_int, [_vp, _vp]),
+    ("slm_plan_layout", _c_int, [_vp, _vp, _vp]),
     ("slm_plan_read_trace", _c_int, [_vp, _c_int, _vp]),
     ("slm_gs", _c_int, [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_double, _vp, _vp, _vp, _vp, _vp]),
     ("slm_gd", _c_int,
@@ -268,7 +269,14 @@ class Plan:
         check(self._lib.slm_plan_info(self.handle, ptr(a)), "slm_plan_info")
         return {"col_cw": int(a[0]), "col_workgroups": int(a[1]), "col_threads": int(a[2]),
                 "row_threads": int(a[3]), "rows_per_workgroup": int(a[4]), "row_plan": int(a[5]),
-                "col_plan": int(a[6]), "precision": "f64" if a[7] == PRECISION_F64 else "f32"}
+                "col_plan": int(a[6]), "precision": "f64" if a[7] == PRECISION_F64 else "f32",
+                "layout": self.layout()}
+
+    def layout(self) -> tuple[int, int]:
+        """(X, Y) panel widths of the plan's blocked device layouts."""
+        x, y = ctypes.c_int(), ctypes.c_int()
+        check(self._lib.slm_plan_layout(self.handle, ctypes.byref(x), ctypes.byref(y)), "slm_plan_layout")
+        return 1 << x.value, 1 << y.value
 
     def read_trace(self, cls: int) -> np.ndarray:
         """[batch * workgroups, 8] phase timestamps of the last launch of a

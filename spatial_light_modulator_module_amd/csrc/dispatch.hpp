@@ -12,8 +12,8 @@ using RowFn = void (*)(RowParams);
 using ColFn = void (*)(ColParams);
 
 #define SLM_DECLARE_LENGTH(N)                    \
-    RowFn row_fn_##N(int mode, int prec);                  \
-    ColFn col_fn_##N(int cw, int mode, int tt, int prec);  \
+    RowFn row_fn_##N(int mode, int prec, int lid);         \
+    ColFn col_fn_##N(int cw, int mode, int tt, int prec, int lid); \
     int row_threads_##N();                       \
     int row_rpw_##N();                           \
     int col_threads_##N(int cw);
@@ -37,15 +37,15 @@ SLM_DECLARE_LENGTH(13)
 static_assert(kNumPlans == 14, "update SLM_DECLARE_LENGTH / SLM_FOR_EACH_LENGTH and the Makefile");
 #define SLM_FOR_EACH_LENGTH(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13)
 
-inline RowFn row_fn(int n, int mode, int prec) {
+inline RowFn row_fn(int n, int mode, int prec, int lid = 0) {
 #define SLM_CASE(N) \
-    case N: return row_fn_##N(mode, prec);
+    case N: return row_fn_##N(mode, prec, lid);
     switch (n) { SLM_FOR_EACH_LENGTH(SLM_CASE) default: return nullptr; }
 #undef SLM_CASE
 }
-inline ColFn col_fn(int n, int cw, int mode, int tt, int prec) {
+inline ColFn col_fn(int n, int cw, int mode, int tt, int prec, int lid = 0) {
 #define SLM_CASE(N) \
-    case N: return col_fn_##N(cw, mode, tt, prec);
+    case N: return col_fn_##N(cw, mode, tt, prec, lid);
     switch (n) { SLM_FOR_EACH_LENGTH(SLM_CASE) default: return nullptr; }
 #undef SLM_CASE
 }

@@ -253,7 +253,22 @@ constexpr int occupancy_wpe(int threads, long long lds_bytes) {
 #ifndef SLM_PANEL_Y_LOG2
 #define SLM_PANEL_Y_LOG2 2
 #endif
-enum Layout : int { LAYOUT_X = SLM_PANEL_X_LOG2, LAYOUT_Y = SLM_PANEL_Y_LOG2 };
+// Layout pairs, chosen per plan (slm_plan_create): 0 = the default panels;
+// 1 = 8-wide X / 2-wide Y for single 1024^2 images on the narrow plan (2-column
+// tiles write whole Y panels, row pairs write 128-B X chunks: 1024^2 GS
+// col 10.31 -> 10.06 us, row 9.50 -> 8.77 us on one box; the batched and
+// 4096 plans measured slower with it: 8 x 4096^2 1317 -> 1405 us).
+enum LayoutId : int { LAYOUT_DEFAULT = 0, LAYOUT_NARROW = 1, kNumLayouts = 2 };
+template <int LID>
+struct LayoutOf {
+    static constexpr int X = LID == LAYOUT_NARROW ? 3 : SLM_PANEL_X_LOG2;
+    static constexpr int Y = LID == LAYOUT_NARROW ? 1 : SLM_PANEL_Y_LOG2;
+};
+__host__ __device__ constexpr int layout_x_log2(int lid) { return lid == LAYOUT_NARROW ? 3 : SLM_PANEL_X_LOG2; }
+__host__ __device__ constexpr int layout_y_log2(int lid) { return lid == LAYOUT_NARROW ? 1 : SLM_PANEL_Y_LOG2; }
+// plans instantiated with the narrow layout pair (plan key 11: 1024 = 8.4.4.8)
+template <int K>
+constexpr bool kHasNarrowLayout = (K == 11);
 template <int PLOG>
 __host__ __device__ __forceinline__ long long blk_index(long long y, int x, int H) {
     return (((long long)(x >> PLOG) * H + y) << PLOG) + (x & ((1 << PLOG) - 1));
@@ -496,8 +511,9 @@ constexpr int row_wpe() {
     return occupancy_wpe(RowCfg<K>::THREADS, (long long)RowCfg<K>::RPW * PlanOf<K>::ROWSTRIDE * sizeof(X));
 }
 
-template <int K, int MODE, int P>
+template <int K, int MODE, int P, int LID>
 __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_kernel(RowParams p) {
+    constexpr int LAYOUT_X = LayoutOf<LID>::X, LAYOUT_Y = LayoutOf<LID>::Y;
     using C = CplxOf<P>;
     using S = Scalar<C>;
     constexpr int W = PlanOf<K>::N;
@@ -655,8 +671,9 @@ constexpr int col_wpe() {
     return occupancy_wpe(ColCfg<K, CW>::THREADS, (long long)PlanOf<K>::LINE * CW * sizeof(X));
 }
 
-template <int K, int CW, int MODE, int TT, int P>
+template <int K, int CW, int MODE, int TT, int P, int LID>
 __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>())) col_kernel(ColParams p) {
+    constexpr int LAYOUT_X = LayoutOf<LID>::X, LAYOUT_Y = LayoutOf<LID>::Y;
     using C = CplxOf<P>;
     using S = Scalar<C>;
     constexpr int H = PlanOf<K>::N;
@@ -910,13 +927,14 @@ __global__ void __launch_bounds__(256) stats_finalize_kernel(StatsParams p) {
 
 // hologram = np.angle(input) of the GD field (src/algorithms.py:111); the
 // field is in the blocked layout, the phase row-major.
+template <int PLOG>
 __global__ void __launch_bounds__(256) field_phase_kernel(const float2* field, float* phase, long long n, int H,
                                                           int W) {
     const long long holo = (long long)H * W;
     for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
         const long long b = i / holo, r = i - b * holo;
         const int y = (int)(r / W), x = (int)(r - (long long)y * W);
-        const float2 f = field[b * holo + blk_index<LAYOUT_Y>(y, x, H)];
+        const float2 f = field[b * holo + blk_index<PLOG>(y, x, H)];
         phase[i] = atan2f(f.y, f.x);
     }
 }

@@ -163,14 +163,24 @@ __global__ void __launch_bounds__(64) target_stats_final_kernel(const double* pa
     }
 }
 
-// layout: LAYOUT_X (X buffers, the target) or LAYOUT_Y (Y, the GD field)
-template <int LAYOUT, typename V>
-int relayout(const V* in, V* out, long long n, int H, int W, bool to_blocked, hipStream_t st) {
+// plog: panel width log2 of the destination / source blocked layout
+// (layout_x_log2(lid): X buffers, the target; layout_y_log2(lid): Y, the GD field)
+template <int PLOG, typename V>
+void relayout_launch(const V* in, V* out, long long n, int H, int W, bool to_blocked, hipStream_t st) {
     const int grid = (int)std::min<long long>(8192, (n + 255) / 256);
     if (to_blocked)
-        hipLaunchKernelGGL((relayout_kernel<V, true, LAYOUT>), dim3(grid), dim3(256), 0, st, in, out, n, H, W);
+        hipLaunchKernelGGL((relayout_kernel<V, true, PLOG>), dim3(grid), dim3(256), 0, st, in, out, n, H, W);
     else
-        hipLaunchKernelGGL((relayout_kernel<V, false, LAYOUT>), dim3(grid), dim3(256), 0, st, in, out, n, H, W);
+        hipLaunchKernelGGL((relayout_kernel<V, false, PLOG>), dim3(grid), dim3(256), 0, st, in, out, n, H, W);
+}
+template <typename V>
+int relayout(int plog, const V* in, V* out, long long n, int H, int W, bool to_blocked, hipStream_t st) {
+    switch (plog) {
+        case 1: relayout_launch<1>(in, out, n, H, W, to_blocked, st); break;
+        case 2: relayout_launch<2>(in, out, n, H, W, to_blocked, st); break;
+        case 3: relayout_launch<3>(in, out, n, H, W, to_blocked, st); break;
+        default: return fail(SLM_ERR_UNSUPPORTED, "no relayout for panel log2 %d", plog);
+    }
     HIP_TRY(hipGetLastError());
     return 0;
 }
@@ -181,6 +191,7 @@ struct slm_plan {
     int algo = 0, B = 0, H = 0, W = 0, tt = 1, has_ain = 0, max_loops = 0;
     int cw = 4, nwg = 0, col_threads = 0, row_threads = 0, rpw = 0;
     int row_key = -1, col_key = -1;  // radix plans (kPlans) of the row / column transforms
+    int lid = -1;                    // blocked layout pair (LayoutId), fixed at the first configure
     int device = 0;
     long long holo = 0;
     hipStream_t stream = nullptr;
@@ -305,6 +316,23 @@ int configure(slm_plan* p, int prec) {
         HIP_TRY(hipGraphExecDestroy(p->gexec));
         p->gexec = nullptr;
     }
+    // layout pair: the narrow one for GS where both transforms have kernels
+    // for it ($SLM_LAYOUT=default forces the default pair). GD keeps the
+    // default: its field round trip through the row pass and its statistics
+    // pass measured slower on the narrow pair (1024^2: 28.9 -> 29.4 us per
+    // iteration, GS 20.9 -> 19.6 us). Device buffers are laid out at upload,
+    // so a plan keeps the pair it was created with.
+    int lid = LAYOUT_DEFAULT;
+    const bool narrow_ok = p->algo == SLM_ALGO_GS && row_fn(row_key, ROW_GS_MAIN, prec, LAYOUT_NARROW) &&
+                           col_fn(col_key, cw, COL_GS_MAIN, TGT_F32, prec, LAYOUT_NARROW);
+    const char* ls = std::getenv("SLM_LAYOUT");
+    if (narrow_ok && !(ls && !std::strcmp(ls, "default"))) lid = LAYOUT_NARROW;
+    if (p->lid >= 0 && lid != p->lid) {
+        if (p->lid == LAYOUT_NARROW && !narrow_ok)
+            return fail(SLM_ERR_UNSUPPORTED, "precision change leaves the plan's layout unsupported");
+        lid = p->lid;
+    }
+    p->lid = lid;
     p->prec = prec;
     p->row_key = row_key;
     p->col_key = col_key;
@@ -410,7 +438,7 @@ int tile_grid(const void* fn, int threads, long long tiles, bool persistent, int
 }
 
 int launch_row(slm_plan* p, int mode, const RowParams& rp, int cls) {
-    RowFn fn = row_fn(p->row_key, mode, p->prec);
+    RowFn fn = row_fn(p->row_key, mode, p->prec, p->lid);
     if (!fn) return fail(SLM_ERR_UNSUPPORTED, "no row kernel for width %d mode %d", p->W, mode);
     RowParams r = rp;
     r.B = p->B;
@@ -423,7 +451,7 @@ int launch_row(slm_plan* p, int mode, const RowParams& rp, int cls) {
 
 int launch_col(slm_plan* p, int mode, const ColParams& cp, int cls) {
     const int tt = (mode == COL_EXPECTED || mode == COL_FFT_FWD || mode == COL_FFT_INV) ? TGT_F32 : p->tt;
-    ColFn fn = col_fn(p->col_key, p->cw, mode, tt, p->prec);
+    ColFn fn = col_fn(p->col_key, p->cw, mode, tt, p->prec, p->lid);
     if (!fn) return fail(SLM_ERR_UNSUPPORTED, "no column kernel for height %d cw %d mode %d", p->H, p->cw, mode);
     ColParams c = cp;
     c.B = p->B;
@@ -529,8 +557,10 @@ int enqueue_gd(slm_plan* p, int loops, double tol, int checked, float wa) {
     {
         const long long n = (long long)p->B * p->holo;
         const int grid = (int)std::min<long long>(4096, (n + 255) / 256);
-        RC(launch(p, SLM_KERNEL_OTHER, field_phase_kernel, dim3(grid), dim3(256), (const float2*)p->field,
-                  p->phase_out, n, p->H, p->W));
+        auto fk = layout_y_log2(p->lid) == 1 ? field_phase_kernel<1>
+                  : layout_y_log2(p->lid) == 3 ? field_phase_kernel<3> : field_phase_kernel<2>;
+        RC(launch(p, SLM_KERNEL_OTHER, fk, dim3(grid), dim3(256), (const float2*)p->field, p->phase_out, n, p->H,
+                  p->W));
     }
     cp.in = p->xa;
     cp.in_alt = p->xb;
@@ -716,11 +746,11 @@ int slm_plan_set_target(slm_plan* p, const void* tgt) {
     if (p->tt == SLM_TGT_U8) {
         hipLaunchKernelGGL(target_stats_partial_kernel<uint8_t>, dim3(kTsBlocks, p->B), dim3(256), 0, p->stream,
                            (const uint8_t*)stage, p->holo, p->ts_part);
-        RC(relayout<LAYOUT_X>((const uint8_t*)stage, (uint8_t*)p->tgt, n, p->H, p->W, true, p->stream));
+        RC(relayout(layout_x_log2(p->lid), (const uint8_t*)stage, (uint8_t*)p->tgt, n, p->H, p->W, true, p->stream));
     } else {
         hipLaunchKernelGGL(target_stats_partial_kernel<float>, dim3(kTsBlocks, p->B), dim3(256), 0, p->stream,
                            (const float*)stage, p->holo, p->ts_part);
-        RC(relayout<LAYOUT_X>((const float*)stage, (float*)p->tgt, n, p->H, p->W, true, p->stream));
+        RC(relayout(layout_x_log2(p->lid), (const float*)stage, (float*)p->tgt, n, p->H, p->W, true, p->stream));
     }
     hipLaunchKernelGGL(target_stats_final_kernel, dim3(p->B), dim3(kTsBlocks), 0, p->stream, p->ts_part, p->norm,
                        p->normf, p->sum_t2);
@@ -779,7 +809,7 @@ int slm_plan_set_field(slm_plan* p, const float* field) {
     }
     const long long n = (long long)p->B * p->holo;
     HIP_TRY(hipMemcpyAsync(p->y, field, (size_t)n * sizeof(float2), hipMemcpyHostToDevice, p->stream));
-    RC(relayout<LAYOUT_Y>((const float2*)p->y, p->field, n, p->H, p->W, true, p->stream));
+    RC(relayout(layout_y_log2(p->lid), (const float2*)p->y, p->field, n, p->H, p->W, true, p->stream));
     HIP_TRY(hipStreamSynchronize(p->stream));
     p->field_set = true;
     return 0;
@@ -930,6 +960,13 @@ int slm_plan_info(slm_plan* p, int* info) {
     return 0;
 }
 
+int slm_plan_layout(slm_plan* p, int* x_log2, int* y_log2) {
+    if (!p || !x_log2 || !y_log2) return fail(SLM_ERR_ARG, "null argument");
+    *x_log2 = layout_x_log2(p->lid);
+    *y_log2 = layout_y_log2(p->lid);
+    return 0;
+}
+
 int slm_gs(const void* tgt, int tgt_type, const float* ain, int batch, int height, int width, int max_loops,
            double tol, const float* init_phase, float* out_phase, float* out_expected, double* out_stats,
            int* out_iters) {
@@ -968,7 +1005,7 @@ int slm_fft2(const float* in, float* out, int batch, int height, int width, int 
     int rc = 0;
     hipError_t e = hipMemcpyAsync(p->y, in, bytes, hipMemcpyHostToDevice, p->stream);
     if (e != hipSuccess) rc = fail(SLM_ERR_HIP, "upload failed: %s", hipGetErrorString(e));
-    if (!rc) rc = relayout<LAYOUT_Y>((const float2*)p->y, p->xa, n, height, width, true, p->stream);  // row-pass input
+    if (!rc) rc = relayout(layout_y_log2(p->lid), (const float2*)p->y, p->xa, n, height, width, true, p->stream);  // row-pass input
     if (!rc) {
         RowParams rp = row_params(p);
         rp.in = p->xa;
@@ -981,7 +1018,7 @@ int slm_fft2(const float* in, float* out, int batch, int height, int width, int 
         cp.out = p->xa;
         rc = launch_col(p, inverse ? COL_FFT_INV : COL_FFT_FWD, cp, SLM_KERNEL_OTHER);
     }
-    if (!rc) rc = relayout<LAYOUT_Y>((const float2*)p->xa, p->y, n, height, width, false, p->stream);  // col-pass output
+    if (!rc) rc = relayout(layout_y_log2(p->lid), (const float2*)p->xa, p->y, n, height, width, false, p->stream);  // col-pass output
     if (!rc) {
         e = hipStreamSynchronize(p->stream);
         if (e == hipSuccess) e = hipMemcpy(out, p->y, bytes, hipMemcpyDeviceToHost);
@@ -1020,7 +1057,7 @@ int slm_plan_read_field(slm_plan* p, float* field) {
     HIP_TRY(hipSetDevice(p->device));
     const long long n = (long long)p->B * p->holo;
     // p->y is scratch between runs (every run rewrites it before reading it)
-    RC(relayout<LAYOUT_Y>((const float2*)p->field, p->y, n, p->H, p->W, false, p->stream));
+    RC(relayout(layout_y_log2(p->lid), (const float2*)p->field, p->y, n, p->H, p->W, false, p->stream));
     HIP_TRY(hipStreamSynchronize(p->stream));
     HIP_TRY(hipMemcpy(field, p->y, (size_t)n * sizeof(float2), hipMemcpyDeviceToHost));
     return 0;

@@ -8,7 +8,9 @@ the plan picker cannot silently move a bench line onto untested kernels:
 * configs[4] per GPU / north star: 4096^2 GS -> narrow 4096 plan (key 13),
   gated at 100 warm-start iterations (SURVEY.md 8c);
 * the column tile widths that give 512- and 1024-thread workgroups (the
-  exchange race fixed in 6e0b072 lived there) against the default tiles.
+  exchange race fixed in 6e0b072 lived there) against the default tiles;
+* the narrow layout pair of single 1024^2 GS images against the default pair
+  (same arithmetic, other addresses: bitwise equal).
 
 Oracle: oracle/fast_f64.py (float64, pinned to the reference goldens in
 tests/test_oracle_golden.py), run on the host's CPU share.
@@ -205,3 +207,31 @@ def test_column_tile_widths(gpu, cw):
         ref5, _, err5 = orc.gerchberg_saxton_faithful(t[0], 5, initial_phase=phi[0])
         assert orc.phase_rms(ph5[0], ref5) < PHASE_RMS_TOL
         np.testing.assert_allclose(st5[0, :5, 3], err5, rtol=1e-5)
+
+
+@pytest.mark.gpu
+def test_gs_1024_layout_pairs_bitwise(gpu):
+    """configs[1] (the bench line) runs on the narrow layout pair (8-wide X,
+    2-wide Y panels); the layout moves addresses only, so phases, expected
+    output and statistics equal the default pair's bit for bit (uint8 and
+    float32 targets, cold and warm start, f32 and f64 butterflies)."""
+    lib = gpu
+    n, loops = 1024, 30
+    t = bench_targets(0, 1, n)
+    phi = np.random.default_rng(7).uniform(-np.pi, np.pi, t.shape).astype(np.float32)
+    for tt, tgt in ((lib.TGT_F32, t), (lib.TGT_U8, np.clip(t, 0, 255).astype(np.uint8))):
+        for prec in (lib.PRECISION_F32, lib.PRECISION_F64):
+            for phase in (None, phi):
+                res = {}
+                for lay in ("narrow", "default"):
+                    with plan_env(SLM_LAYOUT=lay):
+                        with lib.Plan(lib.ALGO_GS, 1, n, n, tt, False, loops) as p:
+                            p.set_precision(prec)
+                            res[lay] = (p.info()["layout"],)
+                            p.set_target(tgt)
+                            p.set_phase(phase)
+                            p.run(loops)
+                            res[lay] += p.read()[:3]
+                assert res["narrow"][0] == (8, 2) and res["default"][0] == (4, 4)
+                for a, b in zip(res["narrow"][1:], res["default"][1:]):
+                    np.testing.assert_array_equal(a, b)
