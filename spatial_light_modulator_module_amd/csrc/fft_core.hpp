@@ -241,35 +241,48 @@ struct Dft<16, INV, C> {
 // ------------------------------------------------------------------------
 // X = float2 or double2: the element type of the exchange (float64 exchanges
 // avoid two conversions per element and pass where the LDS budget allows).
-template <class X>
+// ALT > 0: two exchange buffers ALT elements apart, used alternately. An
+// exchange then needs one barrier (write -> barrier -> read) instead of two:
+// exchange k + 2 rewrites buffer k % 2 only after barrier k + 1, which every
+// wave passes after its reads of exchange k completed (lgkmcnt(0)). `cur` is
+// flipped in fully unrolled code from a constant start, so it folds into the
+// ds_read / ds_write offsets.
+template <class X, int ALT = 0>
 struct LdsLine {  // per-line LDS regions `stride` apart (row kernels)
+    static constexpr bool kDouble = ALT > 0;
     X* base;
     int stride = 0;
+    mutable int cur = 0;
+    __device__ __forceinline__ void flip() const { cur = ALT - cur; }
     template <class C>
     __device__ __forceinline__ void store(int l, int o, C v) const {
-        base[l * stride + o + (o >> 4)] = mk<X>(v.x, v.y);
+        base[cur + l * stride + o + (o >> 4)] = mk<X>(v.x, v.y);
     }
     template <class C>
     __device__ __forceinline__ C load(int l, int o) const {
-        const X v = base[l * stride + o + (o >> 4)];
+        const X v = base[cur + l * stride + o + (o >> 4)];
         return mk<C>(v.x, v.y);
     }
 };
 
-template <int CW, class X>
+template <int CW, class X, int ALT = 0>
 struct LdsTile {  // CW interleaved columns (column kernels): [o][c]; the thread's lines are c + l
+    static constexpr bool kDouble = ALT > 0;
     X* base;
     int c;
+    mutable int cur = 0;
+    __device__ __forceinline__ void flip() const { cur = ALT - cur; }
     template <class C>
     __device__ __forceinline__ void store(int l, int o, C v) const {
-        base[(o + (o >> 4)) * CW + c + l] = mk<X>(v.x, v.y);
+        base[cur + (o + (o >> 4)) * CW + c + l] = mk<X>(v.x, v.y);
     }
     template <class C>
     __device__ __forceinline__ C load(int l, int o) const {
-        const X v = base[(o + (o >> 4)) * CW + c + l];
+        const X v = base[cur + (o + (o >> 4)) * CW + c + l];
         return mk<C>(v.x, v.y);
     }
 };
+
 
 // ------------------------------------------------------------------------
 // Per-thread twiddles. Which twiddles a thread needs depends only on its
@@ -466,6 +479,13 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("" ::: "memory");
 }
 __device__ __forceinline__ void exchange_barrier() { lds_barrier(); }
+template <class Lds>
+__device__ __forceinline__ void exchange_done(const Lds& lds) {
+    if constexpr (Lds::kDouble)
+        lds.flip();
+    else
+        exchange_barrier();
+}
 
 // ------------------------------------------------------------------------
 // Stockham driver.
@@ -540,7 +560,7 @@ __device__ __forceinline__ void stockham_from(V (&v)[L][E], int t, const Tw& tw,
                 v[l][m] = lds.template load<V>(l, t + m * T);
             });
         });
-        exchange_barrier();
+        exchange_done(lds);
         constexpr int kNextReg = RegOff + (Ns > 1 ? NB * (R - 1) : 0);
         constexpr int kNextOff = TwOff + (Ns > 1 ? (R - 1) * Ns : 0);
         constexpr int kNextPow = PowOff + (Ns > 1 ? NB : 0);
@@ -665,7 +685,7 @@ __device__ __forceinline__ void fft_pair(V (&v)[L][PlanOf<K>::E], int t, const T
                 v[l][m] = lds.template load<V>(l, t + m * T);
             });
         });
-        exchange_barrier();
+        exchange_done(lds);
         WriteBack<L, E, V> wb{v};
         stockham_after_first<K, INV2, C>(v, t, tw, lds, wb, RadicesOf<K>{});
     } else {

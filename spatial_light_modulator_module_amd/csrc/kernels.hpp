@@ -505,10 +505,24 @@ __device__ __forceinline__ void tile_loop(long long total, LoadF&& load, ProcF&&
 // ------------------------------------------------------------------------
 // row pass
 // ------------------------------------------------------------------------
+// Double-buffered LDS exchanges (fft_core.hpp, LdsLine / LdsTile ALT): one
+// barrier per exchange instead of two, for twice the exchange LDS. Used where
+// the second buffer leaves the workgroups per CU the launch gets unchanged.
+#ifndef SLM_LDS_DOUBLE
+#define SLM_LDS_DOUBLE 1
+#endif
+// Measured: 1024^2 GS 18.3 -> 17.8 us of kernels per iteration; the 4096 rows
+// (2 x 34 KB per one-row workgroup still fits the two workgroups their VGPRs
+// allow) gained nothing (8 x 4096^2 row pass 799 -> 795 us, one image
+// 100 -> 105 us), and 4096 columns would drop to one workgroup per CU.
+template <int K, bool COL>
+constexpr bool kLdsDouble = SLM_LDS_DOUBLE && K == 11;
+
 template <int K, int P>
 constexpr int row_wpe() {
     using X = XchgOf<P, (long long)RowCfg<K>::RPW * PlanOf<K>::ROWSTRIDE, K>;
-    return occupancy_wpe(RowCfg<K>::THREADS, (long long)RowCfg<K>::RPW * PlanOf<K>::ROWSTRIDE * sizeof(X));
+    return occupancy_wpe(RowCfg<K>::THREADS,
+                         (kLdsDouble<K, false> ? 2 : 1) * (long long)RowCfg<K>::RPW * PlanOf<K>::ROWSTRIDE * sizeof(X));
 }
 
 template <int K, int MODE, int P, int LID>
@@ -525,7 +539,8 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
     constexpr int TL = T < 16 ? T : 16;
     using X = XchgOf<P, (long long)RPW * LINE, K>;
     using V = StateOf<P, X>;
-    __shared__ X smem[RPW * LINE];
+    constexpr int ALT = kLdsDouble<K, false> ? RPW * LINE : 0;
+    __shared__ X smem[(ALT ? 2 : 1) * RPW * LINE];
 
     // lane -> (row group within the quad, transform thread t): TL consecutive
     // t of one row group, then the next group of the quad. One wave instruction
@@ -540,7 +555,7 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
     const int t = tlo + TL * (rest - qq * (T / TL));
     const int lrow = (qq * QR + q4) * L;
     const long long bstep = (long long)T * p.H;  // slot m adds m * bstep (blocked layout)
-    const LdsLine<X> lds{smem + lrow * LINE, LINE};
+    const LdsLine<X, ALT> lds{smem + lrow * LINE, LINE};
     if constexpr (MODE == ROW_GS_MAIN || MODE == ROW_GD_MAIN) trace_entry(p.trace);
     sgpr_pin(p.in, p.out, p.holo, p.H, p.B, p.ntile, p.tw, p.ain, p.wt, gridDim.x);
     Twiddles<K, C, tw_mode<P, RowCfg<K>::THREADS, K, false>()> tw;
@@ -668,7 +683,7 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
 template <int K, int CW, int P>
 constexpr int col_wpe() {
     using X = XchgOf<P, (long long)PlanOf<K>::LINE * CW, K>;
-    return occupancy_wpe(ColCfg<K, CW>::THREADS, (long long)PlanOf<K>::LINE * CW * sizeof(X));
+    return occupancy_wpe(ColCfg<K, CW>::THREADS, (kLdsDouble<K, true> ? 2 : 1) * (long long)PlanOf<K>::LINE * CW * sizeof(X));
 }
 
 template <int K, int CW, int MODE, int TT, int P, int LID>
@@ -684,7 +699,8 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
     constexpr int THREADS = ColCfg<K, CW>::THREADS;
     using X = XchgOf<P, (long long)LINE * CW, K>;
     using V = StateOf<P, X>;
-    __shared__ X smem[LINE * CW];
+    constexpr int ALT = kLdsDouble<K, true> ? LINE * CW : 0;
+    __shared__ X smem[(ALT ? 2 : 1) * LINE * CW];
 
     // a thread carries columns c .. c + L - 1 of the tile (adjacent in the
     // blocked layout: one 16-B access for L = 2)
@@ -693,7 +709,7 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
     // inputs (X, target) in layout X, outputs (Y) in layout Y: row y = t + T m
     constexpr long long kStep = (long long)kPanelOf<LAYOUT_X> * T;
     constexpr long long kStepY = (long long)kPanelOf<LAYOUT_Y> * T;
-    const LdsTile<CW, X> lds{smem, c};
+    const LdsTile<CW, X, ALT> lds{smem, c};
     if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD) trace_entry(p.trace);
     sgpr_pin(p.in, p.out, p.tgt, p.holo, p.nwg, p.B, p.tw, p.checked, p.wt, gridDim.x);
     Twiddles<K, C, tw_mode<P, THREADS, K, true, L>()> tw;
