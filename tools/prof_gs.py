@@ -22,7 +22,7 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--algo", default="gs")
     ap.add_argument("--u8", action="store_true")
-    ap.add_argument("--prec", default="f64")
+    ap.add_argument("--prec", default="f32")  # the library default
     o = ap.parse_args()
     h = o.height or o.size
     w = o.size
