@@ -76,18 +76,20 @@ def targets(first: int, count: int, n: int) -> np.ndarray:
                      for b in range(first, first + count)])
 
 
-def model_bytes(plan, cls):
+def model_bytes(plan, cls, gd_fused=False):
     """SURVEY.md 8d algorithmic bytes per launch (unfused-pass byte model):
     GS 68 B/px/iteration = column passes 32 + target 4 (col_main) + row passes
     32 (row_main); GD 76 = forward column pass 16 (gd_stats) + inverse column
     pass with the target 20 (col_main) + row passes 16 + gradient epilogue 24
-    (row_main). A uint8 target counts 1 B, a_in adds 4 B."""
+    (row_main). When GD's column side is one launch (gd_fused: no gd_stats
+    launches) col_main carries both column passes and the target (36). A uint8
+    target counts 1 B, a_in adds 4 B."""
     px = plan.batch * plan.height * plan.width
     tb = 1 if plan.tgt_type == _lib.TGT_U8 else 4
     ab = 4 if plan.has_ain else 0
     gd = plan.algo == _lib.ALGO_GD
     if cls == _lib.KERNEL_COL_MAIN:
-        return px * ((16 if gd else 32) + tb)
+        return px * ((16 if gd and not gd_fused else 32) + tb)
     if cls == _lib.KERNEL_ROW_MAIN:
         return px * (32 + ab + (8 if gd else 0))
     if cls == _lib.KERNEL_GD_STATS:
@@ -101,13 +103,14 @@ def kernel_roofline(plan, iters, white_attention=0.0):
     roofline numerator, `achieved`) and the bytes the fused kernel physically
     reads and writes (`physical`, slm_plan_kernel_bytes)."""
     us, cnt = plan.run_timed(iters, white_attention=white_attention)
+    gd_fused = plan.algo == _lib.ALGO_GD and cnt[_lib.KERNEL_GD_STATS] == 0
     rows = {}
     for cls in (_lib.KERNEL_COL_MAIN, _lib.KERNEL_ROW_MAIN, _lib.KERNEL_GD_STATS):
         if cnt[cls] == 0:
             continue
         avg_us = us[cls] / cnt[cls]
         phys = plan.kernel_bytes(cls)
-        model = model_bytes(plan, cls)
+        model = model_bytes(plan, cls, gd_fused)
         rows[_lib.KERNEL_CLASS_NAMES[cls]] = {
             "avg_us": avg_us, "launches": int(cnt[cls]), "total_us": float(us[cls]),
             "model_bytes_per_launch": model, "physical_bytes_per_launch": phys,

@@ -43,7 +43,7 @@ extern "C" {
 #define SLM_PRECISION_F64 1 /* float64 butterflies and twiddles */
 
 /* kernel classes for timing / roofline queries */
-#define SLM_KERNEL_COL_MAIN 0 /* GS column pass, or GD gradient column pass */
+#define SLM_KERNEL_COL_MAIN 0 /* GS column pass, or GD column pass (fused statistics + gradient, or the gradient launch) */
 #define SLM_KERNEL_ROW_MAIN 1 /* GS / GD fused row pass */
 #define SLM_KERNEL_GD_STATS 2 /* GD statistics column pass */
 #define SLM_KERNEL_OTHER 3    /* setup, phase extraction, reductions */

@@ -12,10 +12,11 @@
 // 36 B (f32 target) or 33 B (u8 target) instead of 68 B for unfused 2-D FFTs.
 //
 // GD (src/algorithms.py:83-93) needs the global max of |F|^2 before the
-// gradient can be formed, so its column side is two launches (stats, then
-// recompute F and build the gradient) and its row side fuses the inverse row
-// transform, the x/|x| Jacobian-transpose, the update and the next forward row
-// transform.
+// gradient can be formed: its column side is one launch with a grid
+// max-barrier between the forward and the inverse transform where the grid is
+// resident at once (COL_GD_FUSED), else two launches (stats, then recompute F
+// and build the gradient); its row side fuses the inverse row transform, the
+// x/|x| Jacobian-transpose, the update and the next forward row transform.
 #pragma once
 #include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
@@ -73,6 +74,9 @@ struct ColParams {
     const void* tw;          // twiddle table for length H (float2 or double2)
     unsigned long long* trace;  // SLM_TRACE builds: [tile][8] phase timestamps (kTraceSlots)
     int B;                   // holograms
+    double* gresult;         // COL_GD_FUSED: [B][max_loops] hologram max per iteration (kUnset before)
+    double* gslots;          // COL_GD_FUSED: [B][max_loops][nwg] workgroup max per iteration (kUnset before)
+    int* fault;              // COL_GD_FUSED: set when a grid barrier gave up waiting
 };
 
 enum RowMode : int {
@@ -95,7 +99,8 @@ enum ColMode : int {
     COL_GD_GRAD = 4,      // X -> fwd -> mask F (sP - T) -> inv -> Y
     COL_FFT_FWD = 5,      // in -> fwd -> out (test entry)
     COL_FFT_INV = 6,      // in -> inv -> out (test entry)
-    COL_NUM_MODES = 7
+    COL_GD_FUSED = 7,     // X -> fwd -> stats, grid barrier (global max) -> mask F (sP - T) -> inv -> Y
+    COL_NUM_MODES = 8
 };
 
 // target element types: 0 = uint8 (amplitude rounded to float16 as numpy's
@@ -319,6 +324,43 @@ __device__ __forceinline__ void store_field(float2* dst, float2 v, int wt) {
         *dst = v;
 }
 
+// Grid max-barrier of one hologram's column workgroups (COL_GD_FUSED), run by
+// one thread per workgroup after it stored its statistics partials. The host
+// launches that kernel only when every workgroup of the grid is resident at
+// once (occupancy query x CUs >= grid, one tile per workgroup), so every
+// waiter is eventually released; the bounded spin (~0.1 s) is a guard that
+// turns a broken residency assumption into a reported fault, never a hang.
+//
+// Device-scope atomics on one address serialise at the memory side: a flat
+// 512-workgroup counter, and a two-level counter tree, both measured ~13 us
+// from the last arrival to the release (tools/trace_gd.py); (max, generation)
+// slots with a flag measured ~4 us (five dependent memory round trips). So:
+// no atomics and no flags. Every (hologram, iteration) owns a slab of
+// per-workgroup slots and one result word, all preset to the bit pattern
+// kUnset (no |F|^2 maximum is a NaN); a workgroup stores its max into its
+// slot, workgroup 0 of the hologram polls all slots in parallel (one or two
+// per thread), folds them and stores the hologram's max into the result word,
+// which the other workgroups poll. Two dependent memory round trips. Values
+// move with agent-scope (L2-bypassing) 8-byte stores and loads, which are
+// single-copy atomic; no release / acquire fences (those write back and
+// invalidate a whole XCD L2 per workgroup).
+constexpr unsigned long long kUnset = ~0ull;
+
+#ifndef SLM_GRID_SPIN_MAX
+#define SLM_GRID_SPIN_MAX (1 << 21)
+#endif
+#ifndef SLM_GRID_SLEEP
+#define SLM_GRID_SLEEP 8
+#endif
+__device__ __forceinline__ void store_coherent(double* dst, double v) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(dst), __builtin_bit_cast(unsigned long long, v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double load_coherent(const double* src) {
+    return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(src),
+                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
 #ifndef SLM_PREFETCH
 #define SLM_PREFETCH 0  // measured: no gain over one tile per workgroup (the transforms, not the loads, bound a tile)
 #endif
@@ -448,6 +490,50 @@ __device__ __forceinline__ void block_reduce_stats(double& mx, double& s2, doubl
         }
     }
 }
+
+__device__ __forceinline__ unsigned long long load_coherent_bits(const double* src) {
+    return __hip_atomic_load(reinterpret_cast<const unsigned long long*>(src), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+}
+// spin until *src is set; returns its value (kUnset bits -> fault after the guard)
+__device__ __forceinline__ double wait_set(const double* src, int* fault) {
+    unsigned long long v;
+    int spins = 0;
+    while ((v = load_coherent_bits(src)) == kUnset) {
+        __builtin_amdgcn_s_sleep(SLM_GRID_SLEEP);
+        if (++spins > SLM_GRID_SPIN_MAX) {
+            __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return 0.0;
+        }
+    }
+    return __builtin_bit_cast(double, v);
+}
+
+// Global max of one hologram's per-workgroup maxima `mx` (every thread of the
+// workgroup calls it; thread 0's `mx` counts). slots: this (hologram,
+// iteration)'s nwg slots; result: its result word. Returns the max in every thread.
+template <int THREADS>
+__device__ __forceinline__ double grid_max_barrier(double* slots, double* result, double mx, int wg, int nwg,
+                                                   int* fault) {
+    __shared__ double shared_max;
+    lds_barrier();  // the statistics reduction's LDS is reused below
+    if (wg == 0) {
+        double m = threadIdx.x == 0 ? mx : 0.0;
+        for (int k = 1 + threadIdx.x; k < nwg; k += THREADS) m = fmax(m, wait_set(slots + k, fault));
+        double d1 = 0.0, d2 = 0.0;
+        block_reduce_stats<THREADS>(m, d1, d2);
+        if (threadIdx.x == 0) {
+            store_coherent(result, m);
+            shared_max = m;
+        }
+    } else if (threadIdx.x == 0) {
+        store_coherent(slots + wg, mx);
+        shared_max = wait_set(result, fault);
+    }
+    lds_barrier();
+    return shared_max;
+}
+
 
 // state type between passes: complex64 when the exchange is complex64 (see
 // fft_core.hpp, Stockham driver), else the compute type
@@ -710,11 +796,11 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
     constexpr long long kStep = (long long)kPanelOf<LAYOUT_X> * T;
     constexpr long long kStepY = (long long)kPanelOf<LAYOUT_Y> * T;
     const LdsTile<CW, X, ALT> lds{smem, c};
-    if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD) trace_entry(p.trace);
+    if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD || MODE == COL_GD_FUSED) trace_entry(p.trace);
     sgpr_pin(p.in, p.out, p.tgt, p.holo, p.nwg, p.B, p.tw, p.checked, p.wt, gridDim.x);
     Twiddles<K, C, tw_mode<P, THREADS, K, true, L>()> tw;
     load_twiddles<K, C>(tw, t, p.tw);
-    constexpr bool kTarget = (MODE == COL_GS_MAIN || MODE == COL_GD_STATS || MODE == COL_GD_GRAD);
+    constexpr bool kTarget = (MODE == COL_GS_MAIN || MODE == COL_GD_STATS || MODE == COL_GD_GRAD || MODE == COL_GD_FUSED);
     constexpr int NT = kTarget ? E : 1;
 
     // field / target element (row t + T m, column c + l) of a tile at base
@@ -799,7 +885,8 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
         long long base;
         where(tile, b, wg, base);
         const int x = wg * CW + c;
-        unsigned long long* const trace = (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD) ? p.trace : nullptr;
+        unsigned long long* const trace =
+            (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD || MODE == COL_GD_FUSED) ? p.trace : nullptr;
         trace_point(trace, tile, 0, false);
         if constexpr (kTarget) {
             if (p.checked && p.iter > p.stop_iter[b]) return;
@@ -827,6 +914,47 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
             fft_line_epi<K, false, C>(v, t, tw, lds, [&](int l, int m, C& z) {
                 p.e_out[nat + l + (long long)m * T * p.W] = (float)(z.x * z.x + z.y * z.y);
             });
+            return;
+        } else if constexpr (MODE == COL_GD_FUSED) {
+            // GD column side in one launch (src/algorithms.py:84-88): F = fft(X)
+            // and its statistics, a grid barrier for the hologram's global max
+            // of |F|^2, then G = mask F (s|F|^2 - T) and ifft -- F stays in
+            // registers across the barrier instead of being recomputed by a
+            // second launch (COL_GD_STATS + COL_GD_GRAD).
+            double mx = 0.0, s2 = 0.0, st = 0.0;
+            fft_line_epi<K, false, C>(v, t, tw, lds, [&](int l, int m, C& z) {
+                const double ed = (double)(float)(z.x * z.x + z.y * z.y);
+                mx = fmax(mx, ed);
+                s2 += ed * ed;
+                st += ed * (double)tv[l][m];
+            });
+            trace_point(trace, tile, 2, false);
+            block_reduce_stats<THREADS>(mx, s2, st);
+            if (threadIdx.x == 0) {  // the statistics partials (folded after the run by stats_reduce_kernel)
+                double* dst = p.partials + (((long long)b * p.max_loops + p.iter) * p.nwg + wg) * 4;
+                dst[0] = mx;
+                dst[1] = s2;
+                dst[2] = st;
+                dst[3] = 0.0;
+            }
+            const long long it = (long long)b * p.max_loops + p.iter;
+            const double smax = grid_max_barrier<THREADS>(p.gslots + it * p.nwg, p.gresult + it, mx, wg, p.nwg, p.fault);
+            const S maxp = (S)smax;
+            const S norm = (S)p.norm[b];
+            trace_point(trace, tile, 3, true);
+#pragma unroll
+            for (int l = 0; l < L; ++l)
+#pragma unroll
+                for (int mm = 0; mm < E; ++mm) {
+                    const C z = cv<C>(v[l][mm]);
+                    const float tl = tv[l][mm];
+                    const S e = z.x * z.x + z.y * z.y;
+                    const S o = e * norm / maxp;
+                    const S w = ((S)1 + (S)p.wa * (S)tl / (S)255) * (o - (S)tl);
+                    v[l][mm] = cv<V>(mk<C>(z.x * w, z.y * w));
+                }
+            fft_line<K, true, C>(v, t, tw, lds);
+            st_tile(out_base(b, wg), v);
             return;
         } else {
             double mx = 0.0, s2 = 0.0, st = 0.0;

@@ -122,8 +122,7 @@ int get_twiddles(int pk, int prec, const void** out) {
 }
 
 __global__ void fill_int_kernel(int* p, int n, int v) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) p[i] = v;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = v;
 }
 
 // max(T) and sum(T^2) per hologram in double (np.amax(demanded_output),
@@ -214,6 +213,12 @@ struct slm_plan {
     float* phase_out = nullptr;
     float* e_out = nullptr;
     double* partials = nullptr;
+    // COL_GD_FUSED grid max-barrier: [B][max_loops] results, then [B][max_loops][nwg]
+    // workgroup slots (preset to kUnset per run), and a fault flag
+    double* gsync = nullptr;
+    long long gsync_len = 0;
+    int* gfault = nullptr;
+    int gd_fuse = 1;       // $SLM_GD_FUSE at plan creation (0: two-launch GD column side)
     double* stats = nullptr;
     int* stop = nullptr;
     double* norm = nullptr;
@@ -522,6 +527,23 @@ int enqueue_gs(slm_plan* p, int loops, double tol, int checked) {
     return 0;
 }
 
+// GD column side in one launch (COL_GD_FUSED, a grid barrier for the global
+// max of |F|^2) when it is safe and built: unchecked runs (no workgroup leaves
+// early), float32 kernels, and a grid whose workgroups are all resident at once
+// (occupancy x CUs, one tile per workgroup). Otherwise the statistics pass and
+// the gradient pass run as two launches. $SLM_GD_FUSE=0 forces two launches.
+ColFn gd_fused_fn(slm_plan* p, int checked) {
+    if (!p->gd_fuse || !p->gsync || checked || tile_persistent(p->prec, kPlans[p->col_key].e)) return nullptr;
+    ColFn fn = col_fn(p->col_key, p->cw, COL_GD_FUSED, p->tt, p->prec, p->lid);
+    if (!fn) return nullptr;
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)fn, p->col_threads, 0) != hipSuccess)
+        return nullptr;
+    return (long long)p->nwg * p->B <= (long long)per_cu * cus ? fn : nullptr;
+}
+
 int enqueue_gd(slm_plan* p, int loops, double tol, int checked, float wa) {
     RowParams rp = row_params(p);
     ColParams cp = col_params(p);
@@ -540,15 +562,30 @@ int enqueue_gd(slm_plan* p, int loops, double tol, int checked, float wa) {
         rp.out = p->xa;
         RC(launch_row(p, ROW_GD_INIT_Y, rp, SLM_KERNEL_OTHER));
     }
+    const bool fused = gd_fused_fn(p, checked) != nullptr;
+    if (fused) {
+        cp.gresult = p->gsync;
+        cp.gslots = p->gsync + (long long)p->B * p->max_loops;
+        cp.fault = p->gfault;
+        // every result and slot word to kUnset (all bits set) before the run
+        const long long words = 2LL * p->B * p->max_loops * (1 + p->nwg);
+        if (words > INT_MAX) return fail(SLM_ERR_ARG, "grid barrier area too large");
+        RC(launch(p, SLM_KERNEL_OTHER, fill_int_kernel, dim3((int)std::min<long long>(65535, (words + 255) / 256)),
+                  dim3(256), (int*)p->gsync, (int)words, -1));
+    }
     for (int i = 0; i < loops; ++i) {
         float2* xi = (i & 1) ? p->xb : p->xa;
         float2* xn = (i & 1) ? p->xa : p->xb;
         cp.in = xi;
         cp.iter = i;
-        RC(launch_col(p, COL_GD_STATS, cp, SLM_KERNEL_GD_STATS));
-        if (checked) RC(launch_finalize(p, tol, i));
         cp.out = p->y;
-        RC(launch_col(p, COL_GD_GRAD, cp, SLM_KERNEL_COL_MAIN));
+        if (fused) {
+            RC(launch_col(p, COL_GD_FUSED, cp, SLM_KERNEL_COL_MAIN));
+        } else {
+            RC(launch_col(p, COL_GD_STATS, cp, SLM_KERNEL_GD_STATS));
+            if (checked) RC(launch_finalize(p, tol, i));
+            RC(launch_col(p, COL_GD_GRAD, cp, SLM_KERNEL_COL_MAIN));
+        }
         rp.in = p->y;
         rp.out = xn;
         rp.iter = i;
@@ -566,6 +603,18 @@ int enqueue_gd(slm_plan* p, int loops, double tol, int checked, float wa) {
     cp.in_alt = p->xb;
     RC(launch_col(p, COL_EXPECTED, cp, SLM_KERNEL_OTHER));
     return 0;
+}
+
+// A grid barrier of COL_GD_FUSED that gave up waiting (kernels.hpp,
+// grid_arrive_wait) leaves a fault flag: the run's results are invalid.
+int check_grid_fault(slm_plan* p) {
+    if (!p->gfault) return 0;
+    int f = 0;
+    int* flag = p->gfault;
+    HIP_TRY(hipMemcpy(&f, flag, sizeof(int), hipMemcpyDeviceToHost));
+    if (!f) return 0;
+    HIP_TRY(hipMemset(flag, 0, sizeof(int)));
+    return fail(SLM_ERR_HIP, "GD grid barrier timed out (workgroups not co-resident); rerun with SLM_GD_FUSE=0");
 }
 
 int enqueue_run(slm_plan* p, int loops, double tol, int checked, float wa) {
@@ -589,7 +638,8 @@ void free_plan(slm_plan* p) {
     for (void* ptr : {(void*)p->xa, (void*)p->xb, (void*)p->y, (void*)p->field, p->tgt, (void*)p->ain,
                       (void*)p->phase_in, (void*)p->phase_out, (void*)p->e_out, (void*)p->partials,
                       (void*)p->stats, (void*)p->stop, (void*)p->norm, (void*)p->normf, (void*)p->sum_t2,
-                      (void*)p->ts_part, (void*)p->lr, (void*)p->gather_buf, (void*)p->trace_col,
+                      (void*)p->ts_part, (void*)p->lr, (void*)p->gsync, (void*)p->gfault, (void*)p->gather_buf,
+                      (void*)p->trace_col,
                       (void*)p->trace_row})
         if (ptr) (void)hipFree(ptr);
     for (auto& e : p->ev_pool) {
@@ -662,6 +712,7 @@ int slm_plan_create(int algo, int batch, int height, int width, int tgt_type, in
     p->wt_col = height >= 2048 ? 0 : 1;
     p->wt_row = ((long long)batch * p->holo >= (32LL << 20) || width >= 4096) ? 0 : 1;
     if (const char* e = std::getenv("SLM_WT")) p->wt_col = p->wt_row = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SLM_GD_FUSE")) p->gd_fuse = std::atoi(e) != 0;
     if (const char* e = std::getenv("SLM_PRECISION")) p->prec = (std::strcmp(e, "f64") == 0) ? PREC_F64 : PREC_F32;
     // buffers indexed by column panel / row group hold the finer tiling of both precisions
     int max_nwg = 0, min_rpw = INT_MAX;
@@ -700,6 +751,13 @@ int slm_plan_create(int algo, int batch, int height, int width, int tgt_type, in
         RC(alloc((void**)&p->xb, n * sizeof(float2)));
         RC(alloc((void**)&p->field, n * sizeof(float2)));
         RC(alloc((void**)&p->lr, (size_t)max_loops * sizeof(float)));
+        // the one-launch column side needs the whole grid resident: never beyond 8192 workgroups
+        if ((long long)batch * max_nwg <= 8192) {
+            p->gsync_len = (long long)batch * max_loops * (1 + max_nwg);
+            RC(alloc((void**)&p->gsync, (size_t)p->gsync_len * sizeof(double)));
+            RC(alloc((void**)&p->gfault, sizeof(int)));
+            HIP_TRY(hipMemset(p->gfault, 0, sizeof(int)));
+        }
     }
     RC(alloc(&p->tgt, n * tb));
     if (has_ain) RC(alloc((void**)&p->ain, (size_t)p->holo * sizeof(float)));
@@ -872,6 +930,7 @@ int slm_plan_run_timed(slm_plan* p, int loops, double tol, int checked, float wa
     p->timing = false;
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(p->stream));
+    RC(check_grid_fault(p));
     for (int k = 0; k < SLM_NUM_KERNEL_CLASSES; ++k) {
         if (us) us[k] = 0.0;
         if (counts) counts[k] = 0;
@@ -890,13 +949,14 @@ int slm_plan_sync(slm_plan* p) {
     if (!p) return fail(SLM_ERR_ARG, "null plan");
     HIP_TRY(hipSetDevice(p->device));
     HIP_TRY(hipStreamSynchronize(p->stream));
-    return 0;
+    return check_grid_fault(p);
 }
 
 int slm_plan_read(slm_plan* p, float* phase, float* expected, double* stats, int* iters) {
     if (!p) return fail(SLM_ERR_ARG, "null plan");
     HIP_TRY(hipSetDevice(p->device));
     HIP_TRY(hipStreamSynchronize(p->stream));
+    RC(check_grid_fault(p));
     const size_t n = (size_t)p->B * p->holo;
     if (phase) HIP_TRY(hipMemcpy(phase, p->phase_out, n * sizeof(float), hipMemcpyDeviceToHost));
     if (expected) HIP_TRY(hipMemcpy(expected, p->e_out, n * sizeof(float), hipMemcpyDeviceToHost));

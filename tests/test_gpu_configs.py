@@ -10,7 +10,9 @@ the plan picker cannot silently move a bench line onto untested kernels:
 * the column tile widths that give 512- and 1024-thread workgroups (the
   exchange race fixed in 6e0b072 lived there) against the default tiles;
 * the narrow layout pair of single 1024^2 GS images against the default pair
-  (same arithmetic, other addresses: bitwise equal).
+  (same arithmetic, other addresses: bitwise equal);
+* the one-launch GD column side (COL_GD_FUSED, grid barrier for the global
+  max) against the two-launch statistics + gradient passes.
 
 Oracle: oracle/fast_f64.py (float64, pinned to the reference goldens in
 tests/test_oracle_golden.py), run on the host's CPU share.
@@ -235,3 +237,58 @@ def test_gs_1024_layout_pairs_bitwise(gpu):
                 assert res["narrow"][0] == (8, 2) and res["default"][0] == (4, 4)
                 for a, b in zip(res["narrow"][1:], res["default"][1:]):
                     np.testing.assert_array_equal(a, b)
+
+
+def gd_run(lib, t, loops, x0, tt=None, timed=False):
+    b, h, w = t.shape
+    tt = lib.TGT_F32 if tt is None else tt
+    with lib.Plan(lib.ALGO_GD, b, h, w, tt, False, loops) as p:
+        p.set_target(t)
+        p.set_field(x0)
+        p.set_lr(np.full(loops, 0.005, np.float32))
+        cnt = None
+        if timed:
+            _, cnt = p.run_timed(loops, white_attention=1.0)
+        else:
+            p.run(loops, white_attention=1.0)
+        ph, e, stats, _ = p.read()
+        return ph, e, stats[:, :loops], cnt
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,u8", [((1, 1024, 1024), False), ((3, 256, 256), True), ((2, 768, 1024), False)])
+def test_gd_fused_column_pass(gpu, shape, u8):
+    """GD's column side as one launch (COL_GD_FUSED: forward transform and
+    statistics, a grid barrier for the hologram's max |F|^2, gradient and
+    inverse transform on the F still in registers) against the two-launch
+    path ($SLM_GD_FUSE=0: statistics pass, then a gradient pass that recomputes
+    F). Same arithmetic on the same values: phases, expected output and error
+    curves agree to float32 rounding (1e-6 rad rms), both graph-replayed and
+    timed (direct launches), and the timed run shows one column launch per
+    iteration and no statistics launches."""
+    from spatial_light_modulator_module_amd import _lib
+    from spatial_light_modulator_module_amd import algorithms as alg
+
+    lib = gpu
+    b, h, w = shape
+    loops = 60
+    t = bench_targets(0, b, max(h, w))[:, :h, :w]
+    tt = lib.TGT_F32
+    if u8:
+        t = np.clip(t, 0, 255).astype(np.uint8)
+        tt = lib.TGT_U8
+    x0 = np.stack([alg.make_initial_guess("random", None, t[k].astype(np.float64), 42 + k) for k in range(b)])
+    fused = gd_run(lib, t, loops, x0, tt)
+    fused_t = gd_run(lib, t, loops, x0, tt, timed=True)
+    with plan_env(SLM_GD_FUSE=0):
+        two = gd_run(lib, t, loops, x0, tt, timed=True)
+    assert fused_t[3][_lib.KERNEL_GD_STATS] == 0 and fused_t[3][_lib.KERNEL_COL_MAIN] == loops
+    assert two[3][_lib.KERNEL_GD_STATS] == loops and two[3][_lib.KERNEL_COL_MAIN] == loops
+    for k in range(b):
+        rms = orc.phase_rms(fused[0][k], two[0][k])
+        print(f"[parity] GD fused vs two-launch {shape} hologram {k}: phase rms {rms:.3e}, "
+              f"bitwise {np.array_equal(fused[0][k], two[0][k])}")
+        assert rms < 1e-6
+        np.testing.assert_array_equal(fused[0][k], fused_t[0][k])
+    np.testing.assert_allclose(fused[2][..., 3], two[2][..., 3], rtol=1e-5)
+    np.testing.assert_allclose(fused[1], two[1], rtol=1e-3, atol=1e-3 * float(np.max(two[1])))
