@@ -66,7 +66,12 @@ int slm_supported_length(int n);    /* 1 if n is a supported row/column length *
 
 /* ---- plans: device-resident batches ------------------------------------
  * A plan holds `batch` holograms of height x width on the current device.
- * Upload once, run many times (bench), read results.                       */
+ * Upload once, run many times (bench), read results.
+ * GD plans run their column side as one launch with a grid max-barrier when
+ * the whole column grid is resident at once (float32, unchecked runs);
+ * $SLM_GD_FUSE=0 at plan creation forces the two-launch column side. A
+ * barrier that gave up waiting is reported by slm_plan_sync / slm_plan_read /
+ * slm_plan_run_timed as SLM_ERR_HIP (the run's results are invalid).        */
 int slm_plan_create(int algo, int batch, int height, int width, int tgt_type, int has_ain, int max_loops,
                     slm_plan** out);
 int slm_plan_destroy(slm_plan* plan);
