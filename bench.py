@@ -29,6 +29,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import secrets
 import subprocess
 import sys
 import time
@@ -61,10 +62,11 @@ def parse():
 def launch_ranks(n: int) -> int:
     """bench.py --gpus N outside a launcher: N child processes, one per GPU."""
     port = parallel.free_port()
+    token = secrets.token_hex(16)  # admits this job's ranks to the control plane (parallel.job_token)
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SLM_RDZV_PORT=str(port))
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SLM_RDZV_PORT=str(port), SLM_JOB_TOKEN=token)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
     rcs = [p.wait() for p in procs]
     return max(abs(rc) for rc in rcs)
@@ -217,6 +219,8 @@ def secondary(n, batch, iters, algo=_lib.ALGO_GS, precision=None, reps=3):
         dom, rows, _, _ = kernel_roofline(plan, iters, wa)
         info = plan.info()
     iter_s = wall / iters
+    # bytes the launches of one iteration physically move (slm_plan_kernel_bytes)
+    phys_iter = sum(r["physical_bytes_per_launch"] for r in rows.values())
     name = "gd" if algo == _lib.ALGO_GD else "gs"
     traffic = pmc_traffic(f"{name}_{n}x{n}_b{batch}_it{iters}_{info['precision']}")  # rocprofv3 PMC, profiles/
     for k, row in rows.items():
@@ -225,6 +229,7 @@ def secondary(n, batch, iters, algo=_lib.ALGO_GS, precision=None, reps=3):
     return {"algo": name, "shape": [batch, n, n], "iters": iters,
             "holograms_per_s": batch / wall, "iter_ms": iter_s * 1e3, "iter_ms_per_hologram": iter_s * 1e3 / batch,
             "iter_frac_of_hbm_peak_model": round(per_px * batch * n * n / iter_s / 1e9 / HBM_PEAK_GBS, 4),
+            "iter_frac_of_hbm_peak_physical": round(phys_iter / iter_s / 1e9 / HBM_PEAK_GBS, 4),
             "kernels": {k: {kk: _round(vv) for kk, vv in v.items()} for k, v in rows.items()}, "dominant": dom,
             "dominant_frac_of_hbm_peak_model": round(rows[dom]["achieved_gbs"] / HBM_PEAK_GBS, 4),
             "dominant_frac_of_hbm_peak_physical": round(rows[dom]["physical_gbs"] / HBM_PEAK_GBS, 4),
@@ -271,10 +276,17 @@ def main():
 
     dom, rows, _, _ = kernel_roofline(plan, iters)
     info = plan.info()
-    # sanity: the phases are finite and the error curve decreases
-    phase, _, stats, _ = plan.read(expected=False, iters=False)
-    ok = bool(np.isfinite(phase).all() and stats[0, iters - 1, 3] < stats[0, 0, 3])
-    ok = all(group.all_gather(ok))
+    # sanity on rank 0 over EVERY hologram of the job: the gathered phases are
+    # finite and each gathered error curve (slm_plan_gather_stats, the
+    # error_evolution of src/generate_hologram_sequence.py:19-31) decreases
+    gathered = np.empty((bper * world, n, n), np.float32) if rank == 0 else None
+    plan.gather_phase(counts, root=0, host_out=gathered)
+    stats, _ = plan.gather_stats(counts, root=0, want=rank == 0)
+    ok = True
+    if rank == 0:
+        err = stats[:, :iters, 3]
+        ok = bool(np.isfinite(gathered).all() and np.isfinite(err).all() and (err[:, -1] < err[:, 0]).all())
+    ok = group.bcast(ok)
 
     if rank != 0:
         plan.close()
@@ -321,14 +333,14 @@ def main():
     }
     if world == 1 and not opt.no_extra:
         extra = {"pcie_inclusive": pcie_inclusive(plan, targets(0, bper, n), iters)}
-        try:
-            extra["gs_4096"] = secondary(4096, 1, 20)
-            extra["gs_4096_batch8"] = secondary(4096, 8, 20)  # configs[4] per GPU at 8 GPUs
-            extra["gs_1024_batch64"] = secondary(1024, 64, 20)  # configs[3] per GPU at 8 GPUs
+        try:  # every line at its BASELINE.json config's own iteration count
+            extra["gs_4096"] = secondary(4096, 1, 200)  # north-star shape, one hologram
+            extra["gs_4096_batch8"] = secondary(4096, 8, 200)  # configs[4] per GPU at 8 GPUs
+            extra["gs_1024_batch64"] = secondary(1024, 64, 200)  # configs[3] per GPU at 8 GPUs
             extra["gd_1024"] = secondary(1024, 1, 500, algo=_lib.ALGO_GD, reps=2)  # configs[2]
             f64 = _lib.PRECISION_F64  # float64 butterflies (parity margin)
             extra["f64_gs_1024"] = secondary(1024, 1, 200, precision=f64)
-            extra["f64_gs_4096"] = secondary(4096, 1, 20, precision=f64)
+            extra["f64_gs_4096"] = secondary(4096, 1, 200, precision=f64)
         except _lib.SlmError as e:  # pragma: no cover - report, do not hide
             extra["error"] = str(e)
         out["extra"] = extra

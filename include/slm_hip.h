@@ -67,11 +67,14 @@ int slm_supported_length(int n);    /* 1 if n is a supported row/column length *
 /* ---- plans: device-resident batches ------------------------------------
  * A plan holds `batch` holograms of height x width on the current device.
  * Upload once, run many times (bench), read results.
- * GD plans run their column side as one launch with a grid max-barrier when
- * the whole column grid is resident at once (float32, unchecked runs);
- * $SLM_GD_FUSE=0 at plan creation forces the two-launch column side. A
- * barrier that gave up waiting is reported by slm_plan_sync / slm_plan_read /
- * slm_plan_run_timed as SLM_ERR_HIP (the run's results are invalid).        */
+ * GD plans run their column side as one launch that waits for the hologram's
+ * max |F|^2 across workgroups when the whole column grid is resident at once
+ * (float32, unchecked runs), else as two launches; $SLM_GD_MODE=auto|fused|
+ * two|lin at plan creation picks one ($SLM_GD_FUSE=0 = two). If the one-launch
+ * wait ever gives up (other work on the device broke co-residency),
+ * slm_plan_sync / slm_plan_read / slm_plan_run_timed redo that run in-process
+ * on the two-launch path and the plan keeps that path: the caller sees
+ * results, never the fault (slm_plan_gd_recoveries counts such reruns).    */
 int slm_plan_create(int algo, int batch, int height, int width, int tgt_type, int has_ain, int max_loops,
                     slm_plan** out);
 int slm_plan_destroy(slm_plan* plan);
@@ -93,6 +96,7 @@ int slm_plan_run(slm_plan* plan, int loops, double tol, int checked, float white
 int slm_plan_run_timed(slm_plan* plan, int loops, double tol, int checked, float white_attention,
                        double* us_per_class, int* launches_per_class);
 int slm_plan_sync(slm_plan* plan);
+int slm_plan_gd_recoveries(slm_plan* plan); /* GD runs redone after a one-launch wait gave up */
 /* phase [batch][h][w] float32 (radians, angle convention of np.angle);
  * expected [batch][h][w] float32 = |C|^2 of the last iteration (scale by
  * norm / stats[..][0] for expected_outcome); stats [batch][max_loops][4] =
@@ -137,6 +141,18 @@ int slm_gd(const void* tgt, int tgt_type, const float* ain, int batch, int heigh
            double tol, const float* init_field, const float* lr, float white_attention, float* out_phase,
            float* out_expected, double* out_stats, int* out_iters);
 
+/* One process, several GPUs (SURVEY.md 8b's slm_gs_multi): the batch is cut
+ * into n_gpus contiguous shards (the first batch % n_gpus one hologram larger,
+ * as parallel.shard_counts), shard r runs on devices[r] (NULL = 0..n_gpus-1;
+ * a device may repeat) from its own host thread with its own plan and stream,
+ * and lands in its slice of the caller's arrays, each GPU copying over its own
+ * link concurrently. Arguments otherwise as slm_gs; results are bitwise those
+ * of slm_gs on each shard. The reference counterpart is the frame loop of
+ * src/generate_hologram_sequence.py:19-31 run as one batch. */
+int slm_gs_multi(int n_gpus, const int* devices, const void* tgt, int tgt_type, const float* ain, int batch,
+                 int height, int width, int max_loops, double tol, const float* init_phase, float* out_phase,
+                 float* out_expected, double* out_stats, int* out_iters);
+
 /* unscaled 2-D C2C transform of [batch][h][w] complex64 (test entry) */
 int slm_fft2(const float* in_re_im, float* out_re_im, int batch, int height, int width, int inverse);
 
@@ -150,6 +166,17 @@ int slm_comm_destroy(void);
  * the gathered array on the device). Collective; enqueued on the plan stream
  * and synchronised before returning. */
 int slm_plan_gather_phase(slm_plan* plan, const int* counts, int root, float* host_out);
+/* The same collective for the per-iteration statistics that become each
+ * hologram's error_evolution (src/generate_hologram_sequence.py:19-31 keeps one
+ * per frame): on root, stats_out receives sum(counts) x
+ * max_loops x 4 doubles (max E, sum E^2, sum E T, error) and iters_out
+ * sum(counts) ints (iterations executed, -1 = all), rank order; either may be
+ * NULL. */
+int slm_plan_gather_stats(slm_plan* plan, const int* counts, int root, double* stats_out, int* iters_out);
+/* Element offsets of a rank-order gather: offsets[r] = per_item x sum(counts[:r]),
+ * offsets[nranks] = the total (offsets holds nranks + 1 values). The arithmetic
+ * every gather above uses; host-only, needs no device. */
+int slm_gather_layout(int nranks, const int* counts, long long per_item, long long* offsets);
 
 /* ---- SLM frames: trap holograms and 8-bit quantisation ------------------
  * (element-wise, one launch per call, host buffers in/out)

@@ -65,6 +65,7 @@ _SIGNATURES = [
     ("slm_plan_run", _c_int, [_vp, _c_int, _c_double, _c_int, _c_float]),
     ("slm_plan_run_timed", _c_int, [_vp, _c_int, _c_double, _c_int, _c_float, _vp, _vp]),
     ("slm_plan_sync", _c_int, [_vp]),
+    ("slm_plan_gd_recoveries", _c_int, [_vp]),
     ("slm_plan_read", _c_int, [_vp, _vp, _vp, _vp, _vp]),
     ("slm_plan_read_target_stats", _c_int, [_vp, _vp, _vp]),
     ("slm_plan_set_target_stats", _c_int, [_vp, _vp, _vp]),
@@ -77,10 +78,14 @@ _SIGNATURES = [
     ("slm_gd", _c_int,
      [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_double, _vp, _vp, _c_float, _vp, _vp, _vp, _vp]),
     ("slm_fft2", _c_int, [_vp, _vp, _c_int, _c_int, _c_int, _c_int]),
+    ("slm_gs_multi", _c_int, [_c_int, _vp, _vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_double, _vp, _vp,
+                              _vp, _vp, _vp]),
     ("slm_comm_unique_id", _c_int, [_vp]),
     ("slm_comm_init", _c_int, [_c_int, _c_int, _vp]),
     ("slm_comm_destroy", _c_int, []),
     ("slm_plan_gather_phase", _c_int, [_vp, _vp, _c_int, _vp]),
+    ("slm_plan_gather_stats", _c_int, [_vp, _vp, _c_int, _vp, _vp]),
+    ("slm_gather_layout", _c_int, [_c_int, _vp, ctypes.c_longlong, _vp]),
     ("slm_trap_frames", _c_int,
      [_c_int, _c_int, _c_int, _vp, _vp, _vp, _c_double, _c_int, _vp, _vp]),
     ("slm_quantize", _c_int, [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_double, _c_int, _vp]),
@@ -235,6 +240,12 @@ class Plan:
     def sync(self) -> None:
         check(self._lib.slm_plan_sync(self.handle), "slm_plan_sync")
 
+    @property
+    def gd_recoveries(self) -> int:
+        """GD runs redone on the two-launch column side after the one-launch
+        grid wait gave up (slm_plan_gd_recoveries)."""
+        return int(self._lib.slm_plan_gd_recoveries(self.handle))
+
     def read(self, phase=True, expected=True, stats=True, iters=True):
         out_phase = np.empty(self.shape, np.float32) if phase else None
         out_exp = np.empty(self.shape, np.float32) if expected else None
@@ -294,6 +305,17 @@ class Plan:
         c = np.ascontiguousarray(counts, dtype=np.int32)
         check(self._lib.slm_plan_gather_phase(self.handle, ptr(c), root, ptr(host_out)), "slm_plan_gather_phase")
 
+    def gather_stats(self, counts, root: int = 0, want: bool = True):
+        """Every rank's per-iteration statistics [sum(counts)][max_loops][4] and
+        iterations executed [sum(counts)] on `root` (None elsewhere, or when
+        want=False: the collective still runs, nothing is copied to the host)."""
+        c = np.ascontiguousarray(counts, dtype=np.int32)
+        total = int(c.sum())
+        st = np.empty((total, self.max_loops, 4), np.float64) if want else None
+        it = np.empty(total, np.int32) if want else None
+        check(self._lib.slm_plan_gather_stats(self.handle, ptr(c), root, ptr(st), ptr(it)), "slm_plan_gather_stats")
+        return st, it
+
 
 def fft2(x: np.ndarray, inverse: bool = False) -> np.ndarray:
     """Unscaled 2-D C2C transform of [..., H, W] on the GPU (test entry)."""
@@ -337,6 +359,35 @@ def fft2_intensity(phase) -> np.ndarray:
     out = np.empty(a.shape, np.float32)
     init()
     check(load().slm_fft2_intensity(ptr(a), b, h, w, ptr(out)), "slm_fft2_intensity")
+    return out
+
+
+def gs_multi(targets, loops, devices, tol=0.0, ain=None, initial_phase=None):
+    """slm_gs_multi: GS on a batch [B][H][W] sharded over `devices` (device ids,
+    may repeat) from one process. Returns (phase, expected, stats, iters)."""
+    t = np.asarray(targets)
+    tt = TGT_U8 if t.dtype == np.uint8 else TGT_F32
+    t = np.ascontiguousarray(t, dtype=np.uint8 if tt == TGT_U8 else np.float32)
+    b, h, w = t.shape
+    dev = np.ascontiguousarray(devices, dtype=np.int32)
+    a = None if ain is None else np.ascontiguousarray(ain, dtype=np.float32).reshape(h, w)
+    ph0 = None if initial_phase is None else np.ascontiguousarray(initial_phase, dtype=np.float32).reshape(b, h, w)
+    phase = np.empty((b, h, w), np.float32)
+    expected = np.empty((b, h, w), np.float32)
+    stats = np.empty((b, loops, 4), np.float64)
+    iters = np.empty(b, np.int32)
+    init()
+    check(load().slm_gs_multi(int(dev.size), ptr(dev), ptr(t), tt, ptr(a), b, h, w, int(loops), float(tol), ptr(ph0),
+                              ptr(phase), ptr(expected), ptr(stats), ptr(iters)), "slm_gs_multi")
+    return phase, expected, stats, iters
+
+
+def gather_layout(counts, per_item: int) -> np.ndarray:
+    """Rank-order element offsets of a gather (slm_gather_layout; host only):
+    offsets[r] = per_item * sum(counts[:r]), offsets[-1] = the total."""
+    c = np.ascontiguousarray(counts, dtype=np.int32)
+    out = np.empty(c.size + 1, np.int64)
+    check(load().slm_gather_layout(int(c.size), ptr(c), int(per_item), ptr(out)), "slm_gather_layout")
     return out
 
 

@@ -25,6 +25,13 @@
 
 #include "plans.hpp"
 
+#ifndef SLM_LDS_SWZ
+#define SLM_LDS_SWZ 1
+#endif
+#ifndef SLM_COL_LINE_MAJOR
+#define SLM_COL_LINE_MAJOR 1
+#endif
+
 namespace slm {
 
 // ------------------------------------------------------------------------
@@ -60,9 +67,12 @@ struct PlanOf {
     static constexpr int E = kPlans[K].e;
     static constexpr int T = N / E;
     static constexpr int LINE = lds_line(N);
-    // row stride of per-row LDS regions: == 16 (mod 32) complex, so the two rows
-    // served by one 32-lane ds_read_b64 group hit disjoint halves of the banks
-    static constexpr int ROWSTRIDE = LINE + ((16 - LINE % 32) + 32) % 32;
+    // row stride of per-line LDS regions (LdsLine): == 16 (mod 32) complex, so
+    // the two rows served by one 32-lane ds_read_b64 group hit disjoint halves
+    // of the banks. Lines are XOR-swizzled, not padded (SLM_LDS_SWZ), so the
+    // region is N long.
+    static constexpr int LLEN = SLM_LDS_SWZ ? N : LINE;
+    static constexpr int ROWSTRIDE = LLEN + ((16 - LLEN % 32) + 32) % 32;
 };
 
 // cos(2 pi q / 48) for the constant twiddles of radix 2, 3, 4, 8, 12, 16.
@@ -247,8 +257,23 @@ struct Dft<16, INV, C> {
 // wave passes after its reads of exchange k completed (lgkmcnt(0)). `cur` is
 // flipped in fully unrolled code from a constant start, so it folds into the
 // ds_read / ds_write offsets.
+// Element slot of a line in a per-line region. SLM_LDS_SWZ: XOR-swizzle the
+// low 4 index bits with bits 4..7 (a bijection inside each 16-element block):
+// the pass-1 writes (o = 16 t + r), the strided writes of later passes and the
+// lane-contiguous reads (o = t + T m) all hit distinct banks in their
+// 16-lane write / 32-lane read groups (tools/lds_banks.py: 4096 rows 2.0 -> 0
+// extra cycles per read, 768 rows 2.0 -> 0.67 per write, nothing worse).
+// Otherwise one pad slot per 16 (lanes t and t + 16 of a read group collide).
+__device__ __forceinline__ int lds_slot(int o) {
+#if SLM_LDS_SWZ
+    return o ^ ((o >> 4) & 15);
+#else
+    return o + (o >> 4);
+#endif
+}
+
 template <class X, int ALT = 0>
-struct LdsLine {  // per-line LDS regions `stride` apart (row kernels)
+struct LdsLine {  // per-line LDS regions `stride` apart (row kernels; columns of one-group tiles)
     static constexpr bool kDouble = ALT > 0;
     X* base;
     int stride = 0;
@@ -256,11 +281,11 @@ struct LdsLine {  // per-line LDS regions `stride` apart (row kernels)
     __device__ __forceinline__ void flip() const { cur = ALT - cur; }
     template <class C>
     __device__ __forceinline__ void store(int l, int o, C v) const {
-        base[cur + l * stride + o + (o >> 4)] = mk<X>(v.x, v.y);
+        base[cur + l * stride + lds_slot(o)] = mk<X>(v.x, v.y);
     }
     template <class C>
     __device__ __forceinline__ C load(int l, int o) const {
-        const X v = base[cur + l * stride + o + (o >> 4)];
+        const X v = base[cur + l * stride + lds_slot(o)];
         return mk<C>(v.x, v.y);
     }
 };
@@ -268,6 +293,7 @@ struct LdsLine {  // per-line LDS regions `stride` apart (row kernels)
 template <int CW, class X, int ALT = 0>
 struct LdsTile {  // CW interleaved columns (column kernels): [o][c]; the thread's lines are c + l
     static constexpr bool kDouble = ALT > 0;
+    static constexpr int kCW = CW, kAlt = ALT;
     X* base;
     int c;
     mutable int cur = 0;

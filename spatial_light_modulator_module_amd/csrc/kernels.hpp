@@ -37,7 +37,9 @@ struct RowParams {
     const float* ain;        // incoming amplitude [H][W], nullptr = uniform 1
     const float* phase_in;   // warm-start phase [B][H][W]
     float* phase_out;        // output phase [B][H][W]
-    float2* field;           // GD state x [B][H][W]
+    float2* field;           // GD state x [B][H][W] (written)
+    const float2* field_src; // GD state read by this launch: the initial field (iteration 0 of a host-set
+                             // field, which a rerun must find intact) or `field`
     const float* lr;         // GD learning rate per iteration
     const int* stop_iter;    // [B], INT_MAX while running
     int checked;             // tolerance run: honour stop_iter (else it is never read)
@@ -51,6 +53,11 @@ struct RowParams {
     unsigned long long* trace;  // SLM_TRACE builds: [tile][8] phase timestamps (kTraceSlots)
     int B;                   // holograms
     int ntile;               // row groups per hologram (H / rows per workgroup)
+    const float2* in2;       // ROW_GD_LIN: second column-pass output (inverse of mask F T)
+    const double* gmax;      // ROW_GD_LIN: [B][max_loops][nwg_col] column-workgroup maxima of |F|^2
+    const float* norm;       // ROW_GD_LIN: max(T) per hologram
+    int nwg_col;             // ROW_GD_LIN: column workgroups per hologram
+    int max_loops;           // ROW_GD_LIN: gmax slab stride
 };
 
 struct ColParams {
@@ -60,6 +67,7 @@ struct ColParams {
     const void* tgt;         // target intensity T [B][H][W] (uint8 or float)
     double* partials;        // [B][max_loops][nwg] x 4 doubles: max, sum E^2, sum E T, 0
     float* e_out;            // |C|^2 of the final iteration [B][H][W]
+    float* e_blk;            // COL_EXPECTED: |C|^2 in layout Y (relayout to e_out by the host)
     const int* stop_iter;    // [B]
     int checked;             // tolerance run: honour stop_iter (else it is never read)
     const float* norm;       // max(T) per hologram
@@ -76,7 +84,10 @@ struct ColParams {
     int B;                   // holograms
     double* gresult;         // COL_GD_FUSED: [B][max_loops] hologram max per iteration (kUnset before)
     double* gslots;          // COL_GD_FUSED: [B][max_loops][nwg] workgroup max per iteration (kUnset before)
-    int* fault;              // COL_GD_FUSED: set when a grid barrier gave up waiting
+    int* fault;              // COL_GD_FUSED: set when a grid wait gave up
+    int skip_wg_plus1;       // COL_GD_FUSED test knob: workgroup (value - 1) never publishes (0 = off)
+    float2* out2;            // COL_GD_LIN: second output (inverse column transform of mask F T)
+    double* gmax;            // COL_GD_LIN: [B][max_loops][nwg] workgroup maxima of |F|^2 (dense)
 };
 
 enum RowMode : int {
@@ -88,7 +99,8 @@ enum RowMode : int {
     ROW_GD_MAIN = 5,      // Y -> inv -> gradient, update field -> fwd -> X
     ROW_FFT_FWD = 6,      // in -> fwd -> out (test entry)
     ROW_FFT_INV = 7,      // in -> inv -> out (test entry)
-    ROW_NUM_MODES = 8
+    ROW_GD_LIN = 8,       // s U - V (s from the column maxima) -> inv -> gradient, update field -> fwd -> X
+    ROW_NUM_MODES = 9
 };
 
 enum ColMode : int {
@@ -100,7 +112,8 @@ enum ColMode : int {
     COL_FFT_FWD = 5,      // in -> fwd -> out (test entry)
     COL_FFT_INV = 6,      // in -> inv -> out (test entry)
     COL_GD_FUSED = 7,     // X -> fwd -> stats, grid barrier (global max) -> mask F (sP - T) -> inv -> Y
-    COL_NUM_MODES = 8
+    COL_GD_LIN = 8,       // X -> fwd -> stats; mask F P -> inv -> Y, mask F T -> inv -> Y2 (no global max needed)
+    COL_NUM_MODES = 9
 };
 
 // target element types: 0 = uint8 (amplitude rounded to float16 as numpy's
@@ -328,8 +341,10 @@ __device__ __forceinline__ void store_field(float2* dst, float2 v, int wt) {
 // one thread per workgroup after it stored its statistics partials. The host
 // launches that kernel only when every workgroup of the grid is resident at
 // once (occupancy query x CUs >= grid, one tile per workgroup), so every
-// waiter is eventually released; the bounded spin (~0.1 s) is a guard that
-// turns a broken residency assumption into a reported fault, never a hang.
+// waiter is eventually released; the bounded spin (2^21 polls of s_sleep 8,
+// about 0.5-1.5 s) is a guard that turns a broken residency assumption into a
+// fault flag, never a hang: later waits of the run leave at once, and the host
+// redoes the run on the two-launch path (slm_capi.hip, recover_grid_fault).
 //
 // Device-scope atomics on one address serialise at the memory side: a flat
 // 512-workgroup counter, and a two-level counter tree, both measured ~13 us
@@ -343,7 +358,11 @@ __device__ __forceinline__ void store_field(float2* dst, float2 v, int wt) {
 // which the other workgroups poll. Two dependent memory round trips. Values
 // move with agent-scope (L2-bypassing) 8-byte stores and loads, which are
 // single-copy atomic; no release / acquire fences (those write back and
-// invalidate a whole XCD L2 per workgroup).
+// invalidate a whole XCD L2 per workgroup). Measured alternatives (GD 1024^2,
+// per fused launch): every workgroup polling the whole slab itself (one round
+// trip, 512 x 512 polls) 16.6 us against 14.3 us; overlapping the wait with
+// the inverse transforms of the split gradient (s U - V, see COL_GD_LIN) did
+// not hide it -- the last arrivals trail the first by several microseconds.
 constexpr unsigned long long kUnset = ~0ull;
 
 #ifndef SLM_GRID_SPIN_MAX
@@ -495,11 +514,15 @@ __device__ __forceinline__ unsigned long long load_coherent_bits(const double* s
     return __hip_atomic_load(reinterpret_cast<const unsigned long long*>(src), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
 }
-// spin until *src is set; returns its value (kUnset bits -> fault after the guard)
+// spin until *src is set; returns its value. Gives up (and raises the fault
+// flag) after the guard, or as soon as another waiter has raised it: once one
+// barrier of the run has failed every later wait returns at once, so a broken
+// residency assumption costs one guard interval, not one per iteration.
 __device__ __forceinline__ double wait_set(const double* src, int* fault) {
     unsigned long long v;
     int spins = 0;
     while ((v = load_coherent_bits(src)) == kUnset) {
+        if ((spins & 63) == 0 && __hip_atomic_load(fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return 0.0;
         __builtin_amdgcn_s_sleep(SLM_GRID_SLEEP);
         if (++spins > SLM_GRID_SPIN_MAX) {
             __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -511,10 +534,12 @@ __device__ __forceinline__ double wait_set(const double* src, int* fault) {
 
 // Global max of one hologram's per-workgroup maxima `mx` (every thread of the
 // workgroup calls it; thread 0's `mx` counts). slots: this (hologram,
-// iteration)'s nwg slots; result: its result word. Returns the max in every thread.
+// iteration)'s nwg slots; result: its result word. Returns the max in every
+// thread (0 after a fault: the host then discards the run). skip_wg_plus1 - 1
+// is a workgroup that never publishes (fault-path test knob; 0 = none).
 template <int THREADS>
 __device__ __forceinline__ double grid_max_barrier(double* slots, double* result, double mx, int wg, int nwg,
-                                                   int* fault) {
+                                                   int* fault, int skip_wg_plus1) {
     __shared__ double shared_max;
     lds_barrier();  // the statistics reduction's LDS is reused below
     if (wg == 0) {
@@ -527,13 +552,12 @@ __device__ __forceinline__ double grid_max_barrier(double* slots, double* result
             shared_max = m;
         }
     } else if (threadIdx.x == 0) {
-        store_coherent(slots + wg, mx);
+        if (wg + 1 != skip_wg_plus1) store_coherent(slots + wg, mx);
         shared_max = wait_set(result, fault);
     }
     lds_barrier();
     return shared_max;
 }
-
 
 // state type between passes: complex64 when the exchange is complex64 (see
 // fft_core.hpp, Stockham driver), else the compute type
@@ -642,7 +666,7 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
     const int lrow = (qq * QR + q4) * L;
     const long long bstep = (long long)T * p.H;  // slot m adds m * bstep (blocked layout)
     const LdsLine<X, ALT> lds{smem + lrow * LINE, LINE};
-    if constexpr (MODE == ROW_GS_MAIN || MODE == ROW_GD_MAIN) trace_entry(p.trace);
+    if constexpr (MODE == ROW_GS_MAIN || MODE == ROW_GD_MAIN || MODE == ROW_GD_LIN) trace_entry(p.trace);
     sgpr_pin(p.in, p.out, p.holo, p.H, p.B, p.ntile, p.tw, p.ain, p.wt, gridDim.x);
     Twiddles<K, C, tw_mode<P, RowCfg<K>::THREADS, K, false>()> tw;
     load_twiddles<K, C>(tw, t, p.tw);
@@ -680,7 +704,7 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
             } else if constexpr (MODE == ROW_GD_INIT_FIELD) {
 #pragma unroll
                 for (int m = 0; m < E; ++m)
-                    v[l][m] = cv<V>(normalize(from_c64<C>(p.field[boff + PY * l + m * bstep]), ain_at(l, m)));
+                    v[l][m] = cv<V>(normalize(from_c64<C>(p.field_src[boff + PY * l + m * bstep]), ain_at(l, m)));
             } else {
 #pragma unroll
                 for (int m = 0; m < E; ++m) v[l][m] = cv<V>(p.in[boff + PY * l + m * bstep]);
@@ -693,12 +717,13 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
         where(tile, b, hoff, roff, boff, xoff);
         auto ain_at = [&](int l, int m) -> S { return p.ain ? (S)p.ain[roff + l * W + t + T * m] : (S)1; };
         // timeline of the iteration launches only (SLM_TRACE)
-        unsigned long long* const trace = (MODE == ROW_GS_MAIN || MODE == ROW_GD_MAIN) ? p.trace : nullptr;
+        unsigned long long* const trace =
+            (MODE == ROW_GS_MAIN || MODE == ROW_GD_MAIN || MODE == ROW_GD_LIN) ? p.trace : nullptr;
         trace_point(trace, tile, 0, false);
         // (unchecked runs never stop early: no dependent load of the flag)
         if constexpr (MODE == ROW_GS_MAIN) {
             if (p.checked && p.iter >= p.stop_iter[b]) return;  // stopped after this iteration's column pass
-        } else if constexpr (MODE == ROW_GD_MAIN) {
+        } else if constexpr (MODE == ROW_GD_MAIN || MODE == ROW_GD_LIN) {
             if (p.checked && p.iter > p.stop_iter[b]) return;
         }
         trace_point(trace, tile, 1, true);
@@ -730,7 +755,7 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
                 const S a = ain_at(l, m);
                 const C g = mk<C>(z.x * inv_s * a, z.y * inv_s * a);
                 const long long idx = boff + PY * l + m * bstep;
-                C x = from_c64<C>(p.field[idx]);
+                C x = from_c64<C>(p.field_src[idx]);  // (loaded here: a prefetch at tile start measured no faster)
                 const S ax2 = x.x * x.x + x.y * x.y;
                 const S inv = rsqrt_nr(ax2);
                 const S inv3 = inv * inv * inv;
@@ -741,6 +766,56 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
                 x.y -= lr * dy;
                 const float2 xs = to_c64(x);  // the field is stored in complex64
                 p.field[idx] = xs;
+                z = normalize(from_c64<C>(xs), a);
+            });
+        } else if constexpr (MODE == ROW_GD_LIN) {
+            // The column pass left U = ifft_col(mask F P) and V = ifft_col(mask F T);
+            // ifft_col(mask F (s P - T)) = s U - V with s = norm / max |F|^2 of this
+            // iteration (src/algorithms.py:85-88), reduced here from the column
+            // workgroups' maxima -- no grid-wide barrier inside a launch.
+            V q[L][E];
+            float2 xf[L][E];
+#pragma unroll
+            for (int l = 0; l < L; ++l)
+#pragma unroll
+                for (int m = 0; m < E; ++m) {
+                    q[l][m] = cv<V>(p.in2[boff + PY * l + m * bstep]);
+                    xf[l][m] = p.field_src[boff + PY * l + m * bstep];  // fetched with the inputs, used after the inverse
+                }
+            __shared__ double smax;
+            {
+                const double* gm = p.gmax + ((long long)b * p.max_loops + p.iter) * p.nwg_col;
+                double mx = 0.0, d1 = 0.0, d2 = 0.0;
+                for (int k = threadIdx.x; k < p.nwg_col; k += RowCfg<K>::THREADS) mx = fmax(mx, gm[k]);
+                block_reduce_stats<RowCfg<K>::THREADS>(mx, d1, d2);
+                if (threadIdx.x == 0) smax = mx;
+                lds_barrier();
+            }
+            const S s = (S)p.norm[b] / (S)smax;
+#pragma unroll
+            for (int l = 0; l < L; ++l)
+#pragma unroll
+                for (int m = 0; m < E; ++m) {
+                    const C u = cv<C>(v[l][m]), w = cv<C>(q[l][m]);
+                    v[l][m] = cv<V>(mk<C>(s * u.x - w.x, s * u.y - w.y));
+                }
+            const S lr = (S)p.lr[p.iter];
+            const S inv_s = (S)1 / (S)p.holo;
+            fft_pair<K, true, false, C>(v, t, tw, lds, [&](int l, int m, C& z) {
+                // dEdF = ifft2(...) * a_in (:87-89); dEdX_complex (:179-185); x -= lr dEdX (:91)
+                const S a = ain_at(l, m);
+                const C g = mk<C>(z.x * inv_s * a, z.y * inv_s * a);
+                C x = from_c64<C>(xf[l][m]);
+                const S ax2 = x.x * x.x + x.y * x.y;
+                const S inv = rsqrt_nr(ax2);
+                const S inv3 = inv * inv * inv;
+                const S re = x.x * g.x + x.y * g.y;
+                const S dx = g.x * inv - x.x * re * inv3;
+                const S dy = g.y * inv - x.y * re * inv3;
+                x.x -= lr * dx;
+                x.y -= lr * dy;
+                const float2 xs = to_c64(x);
+                p.field[boff + PY * l + m * bstep] = xs;
                 z = normalize(from_c64<C>(xs), a);
             });
         }
@@ -766,14 +841,89 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
 // ------------------------------------------------------------------------
 // column pass
 // ------------------------------------------------------------------------
-template <int K, int CW, int P>
+// The two terms of the split GD gradient (src/algorithms.py:80,85-88):
+// mask F |F|^2 and mask F T, mask = 1 + wa T / 255, from F in the slots.
+template <class C, class V, class TV, int L, int E>
+__device__ __forceinline__ void gd_split_terms(const V (&v)[L][E], const TV (&tv)[L][E], Scalar<C> wa, V (&wu)[L][E],
+                                               V (&wv)[L][E]) {
+    using S = Scalar<C>;
+#pragma unroll
+    for (int l = 0; l < L; ++l)
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const C z = cv<C>(v[l][m]);
+            const float tl = tv[l][m];
+            const S e = z.x * z.x + z.y * z.y;
+            const S mask = (S)1 + wa * (S)tl / (S)255;
+            const S a = mask * e, q = mask * (S)tl;
+            wu[l][m] = cv<V>(mk<C>(z.x * a, z.y * a));
+            wv[l][m] = cv<V>(mk<C>(z.x * q, z.y * q));
+        }
+}
+
+// Inverse column transforms of both terms: as 2 L lines through one exchange
+// region of 2 CW columns (DUAL: shared twiddles and barriers), else one after
+// the other through the kernel's own region.
+template <int K, class C, bool DUAL, class V, int L, int E, class Tw, class Lds, class X>
+__device__ __forceinline__ void gd_inverse_pair(V (&wu)[L][E], V (&wv)[L][E], int t, const Tw& tw, const Lds& lds,
+                                                X* smem, int c) {
+    if constexpr (DUAL) {
+        V w2[2 * L][E];
+#pragma unroll
+        for (int l = 0; l < L; ++l)
+#pragma unroll
+            for (int m = 0; m < E; ++m) {
+                w2[l][m] = wu[l][m];
+                w2[L + l][m] = wv[l][m];
+            }
+        // the same buffer alternation continues (kDouble exchanges)
+        const LdsTile<2 * Lds::kCW, X, Lds::kAlt> lds2{smem, 2 * c, lds.cur};
+        fft_line<K, true, C>(w2, t, tw, lds2);
+#pragma unroll
+        for (int l = 0; l < L; ++l)
+#pragma unroll
+            for (int m = 0; m < E; ++m) {
+                wu[l][m] = w2[l][m];
+                wv[l][m] = w2[L + l][m];
+            }
+    } else {
+        fft_line<K, true, C>(wu, t, tw, lds);
+        fft_line<K, true, C>(wv, t, tw, lds);
+    }
+}
+
+// COL_GD_LIN runs its two inverse column transforms (mask F P and mask F T)
+// as two lines per column of the thread, sharing twiddles and
+// exchange barriers, where the doubled exchange region still leaves two
+// workgroups per CU; else one after the other through the same region.
+// Column tiles whose threads carry every column of the tile (CW == L: the
+// 4096 narrow plan, two columns per thread) exchange through line-major
+// swizzled regions instead of the [o][c] interleave: an instruction then
+// touches one line only, and the interleave's stride-2 slots cost 4 / 2 extra
+// cycles per write / read (tools/lds_banks.py).
+template <int K, int CW>
+constexpr bool kColLineMajor = SLM_COL_LINE_MAJOR && ColCfg<K, CW>::L == CW;
+
+template <int K, int CW, int P, int MODE>
+constexpr bool kColDualInv() {
+    using X = XchgOf<P, (long long)PlanOf<K>::LINE * CW, K>;
+    return MODE == COL_GD_LIN && !kColLineMajor<K, CW> &&
+           (kLdsDouble<K, true> ? 2 : 1) * (long long)PlanOf<K>::LINE * 2 * CW * sizeof(X) <= kLdsPair;
+}
+template <int K, int CW, int P, int MODE>
+constexpr int col_lds_width() {
+    return kColDualInv<K, CW, P, MODE>() ? 2 * CW : CW;
+}
+
+template <int K, int CW, int P, int MODE = COL_GS_MAIN>
 constexpr int col_wpe() {
     using X = XchgOf<P, (long long)PlanOf<K>::LINE * CW, K>;
-    return occupancy_wpe(ColCfg<K, CW>::THREADS, (kLdsDouble<K, true> ? 2 : 1) * (long long)PlanOf<K>::LINE * CW * sizeof(X));
+    return occupancy_wpe(ColCfg<K, CW>::THREADS, (kLdsDouble<K, true> ? 2 : 1) * (long long)PlanOf<K>::LINE *
+                                                     col_lds_width<K, CW, P, MODE>() * sizeof(X));
 }
 
 template <int K, int CW, int MODE, int TT, int P, int LID>
-__global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>())) col_kernel(ColParams p) {
+__global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P, MODE>())) col_kernel(ColParams p) {
     constexpr int LAYOUT_X = LayoutOf<LID>::X, LAYOUT_Y = LayoutOf<LID>::Y;
     using C = CplxOf<P>;
     using S = Scalar<C>;
@@ -785,8 +935,9 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
     constexpr int THREADS = ColCfg<K, CW>::THREADS;
     using X = XchgOf<P, (long long)LINE * CW, K>;
     using V = StateOf<P, X>;
-    constexpr int ALT = kLdsDouble<K, true> ? LINE * CW : 0;
-    __shared__ X smem[(ALT ? 2 : 1) * LINE * CW];
+    constexpr int LW = col_lds_width<K, CW, P, MODE>();  // exchange columns (2 CW: COL_GD_LIN's paired inverses)
+    constexpr int ALT = kLdsDouble<K, true> ? LINE * LW : 0;
+    __shared__ X smem[(ALT ? 2 : 1) * LINE * LW];
 
     // a thread carries columns c .. c + L - 1 of the tile (adjacent in the
     // blocked layout: one 16-B access for L = 2)
@@ -795,12 +946,21 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
     // inputs (X, target) in layout X, outputs (Y) in layout Y: row y = t + T m
     constexpr long long kStep = (long long)kPanelOf<LAYOUT_X> * T;
     constexpr long long kStepY = (long long)kPanelOf<LAYOUT_Y> * T;
-    const LdsTile<CW, X, ALT> lds{smem, c};
-    if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD || MODE == COL_GD_FUSED) trace_entry(p.trace);
+    using LdsT = std::conditional_t<kColLineMajor<K, CW>, LdsLine<X, ALT>, LdsTile<CW, X, ALT>>;
+    static_assert(!kColLineMajor<K, CW> || PlanOf<K>::ROWSTRIDE * CW <= LINE * LW, "line-major region fits");
+    const LdsT lds = [&] {
+        if constexpr (kColLineMajor<K, CW>)
+            return LdsT{smem, PlanOf<K>::ROWSTRIDE};  // c == 0: the thread's lines are its columns
+        else
+            return LdsT{smem, c};
+    }();
+    if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD || MODE == COL_GD_FUSED || MODE == COL_GD_LIN)
+        trace_entry(p.trace);
     sgpr_pin(p.in, p.out, p.tgt, p.holo, p.nwg, p.B, p.tw, p.checked, p.wt, gridDim.x);
     Twiddles<K, C, tw_mode<P, THREADS, K, true, L>()> tw;
     load_twiddles<K, C>(tw, t, p.tw);
-    constexpr bool kTarget = (MODE == COL_GS_MAIN || MODE == COL_GD_STATS || MODE == COL_GD_GRAD || MODE == COL_GD_FUSED);
+    constexpr bool kTarget = (MODE == COL_GS_MAIN || MODE == COL_GD_STATS || MODE == COL_GD_GRAD ||
+                              MODE == COL_GD_FUSED || MODE == COL_GD_LIN);
     constexpr int NT = kTarget ? E : 1;
 
     // field / target element (row t + T m, column c + l) of a tile at base
@@ -824,24 +984,25 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
         }
     };
     // stores of a whole tile (layout Y); `wt` is uniform, so it branches once per tile
-    auto st_tile = [&](long long base, const V (&v)[L][E]) {
+    auto st_tile_to = [&](float2* dst, long long base, const V (&v)[L][E]) {
         if (p.wt) {
 #pragma unroll
             for (int m = 0; m < E; ++m)
 #pragma unroll
-                for (int l = 0; l < L; ++l) store_field(p.out + base + m * kStepY + l, cv<float2>(v[l][m]), 1);
+                for (int l = 0; l < L; ++l) store_field(dst + base + m * kStepY + l, cv<float2>(v[l][m]), 1);
         } else {
 #pragma unroll
             for (int m = 0; m < E; ++m) {
                 if constexpr (L == 2) {
                     const float2 a = cv<float2>(v[0][m]), b = cv<float2>(v[1][m]);
-                    *reinterpret_cast<float4*>(p.out + base + m * kStepY) = make_float4(a.x, a.y, b.x, b.y);
+                    *reinterpret_cast<float4*>(dst + base + m * kStepY) = make_float4(a.x, a.y, b.x, b.y);
                 } else {
-                    p.out[base + m * kStepY] = cv<float2>(v[0][m]);
+                    dst[base + m * kStepY] = cv<float2>(v[0][m]);
                 }
             }
         }
     };
+    auto st_tile = [&](long long base, const V (&v)[L][E]) { st_tile_to(p.out, base, v); };
 
     // tile = (hologram b, column group wg); element (y, x) at blk_index<layout>(y, x, H)
     auto where = [&](long long tile, int& b, int& wg, long long& base) {
@@ -884,9 +1045,9 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
         int b, wg;
         long long base;
         where(tile, b, wg, base);
-        const int x = wg * CW + c;
         unsigned long long* const trace =
-            (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD || MODE == COL_GD_FUSED) ? p.trace : nullptr;
+            (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD || MODE == COL_GD_FUSED || MODE == COL_GD_LIN) ? p.trace
+                                                                                                       : nullptr;
         trace_point(trace, tile, 0, false);
         if constexpr (kTarget) {
             if (p.checked && p.iter > p.stop_iter[b]) return;
@@ -910,10 +1071,44 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
             st_tile(out_base(b, wg), v);
             return;
         } else if constexpr (MODE == COL_EXPECTED) {
-            const long long nat = (long long)b * p.holo + (long long)t * p.W + x;  // row-major output
+            // |C|^2 in layout Y (a column tile's stores are whole panel runs, like the
+            // field's); the host relayouts it to the row-major e_out afterwards --
+            // row-major stores from a column tile were one 4-B segment per lane
+            const long long ob = out_base(b, wg);
             fft_line_epi<K, false, C>(v, t, tw, lds, [&](int l, int m, C& z) {
-                p.e_out[nat + l + (long long)m * T * p.W] = (float)(z.x * z.x + z.y * z.y);
+                p.e_blk[ob + m * kStepY + l] = (float)(z.x * z.x + z.y * z.y);
             });
+            return;
+        } else if constexpr (MODE == COL_GD_LIN) {
+            // GD column side with no global max inside the launch (src/algorithms.py:84-88):
+            // G = mask F (s |F|^2 - T) = s (mask F |F|^2) - (mask F T), s = norm / max |F|^2.
+            // Both terms are inverse-transformed along the columns here (Y, Y2); the row
+            // pass forms s U - V once every column workgroup's max is in memory.
+            double mx = 0.0, s2 = 0.0, st = 0.0;
+            fft_line_epi<K, false, C>(v, t, tw, lds, [&](int l, int m, C& z) {
+                const double ed = (double)(float)(z.x * z.x + z.y * z.y);
+                mx = fmax(mx, ed);
+                s2 += ed * ed;
+                st += ed * (double)tv[l][m];
+            });
+            trace_point(trace, tile, 2, false);
+            V wu[L][E], wv[L][E];
+            gd_split_terms<C>(v, tv, (S)p.wa, wu, wv);
+            gd_inverse_pair<K, C, LW == 2 * CW>(wu, wv, t, tw, lds, smem, c);
+            const long long ob = out_base(b, wg);
+            st_tile_to(p.out, ob, wu);
+            st_tile_to(p.out2, ob, wv);
+            block_reduce_stats<THREADS>(mx, s2, st);
+            if (threadIdx.x == 0) {
+                const long long it = (long long)b * p.max_loops + p.iter;
+                double* dst = p.partials + (it * p.nwg + wg) * 4;
+                dst[0] = mx;
+                dst[1] = s2;
+                dst[2] = st;
+                dst[3] = 0.0;
+                p.gmax[it * p.nwg + wg] = mx;
+            }
+            trace_point(trace, tile, 3, true);
             return;
         } else if constexpr (MODE == COL_GD_FUSED) {
             // GD column side in one launch (src/algorithms.py:84-88): F = fft(X)
@@ -938,7 +1133,8 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P>()
                 dst[3] = 0.0;
             }
             const long long it = (long long)b * p.max_loops + p.iter;
-            const double smax = grid_max_barrier<THREADS>(p.gslots + it * p.nwg, p.gresult + it, mx, wg, p.nwg, p.fault);
+            const double smax = grid_max_barrier<THREADS>(p.gslots + it * p.nwg, p.gresult + it, mx, wg, p.nwg,
+                                                          p.fault, p.skip_wg_plus1);
             const S maxp = (S)smax;
             const S norm = (S)p.norm[b];
             trace_point(trace, tile, 3, true);

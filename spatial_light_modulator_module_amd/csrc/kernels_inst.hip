@@ -25,6 +25,7 @@ RowFn row_table(int mode) {
         case ROW_GD_MAIN: return row_kernel<N, ROW_GD_MAIN, P, LID>;
         case ROW_FFT_FWD: return row_kernel<N, ROW_FFT_FWD, P, LID>;
         case ROW_FFT_INV: return row_kernel<N, ROW_FFT_INV, P, LID>;
+        case ROW_GD_LIN: return row_kernel<N, ROW_GD_LIN, P, LID>;
         default: return nullptr;
     }
 }
@@ -49,6 +50,8 @@ ColFn col_table_cw(int mode, int tt) {
                     return u8 ? col_kernel<N, CW, COL_GD_FUSED, TGT_U8, P, LID> : col_kernel<N, CW, COL_GD_FUSED, TGT_F32, P, LID>;
                 else
                     return nullptr;
+            case COL_GD_LIN:
+                return u8 ? col_kernel<N, CW, COL_GD_LIN, TGT_U8, P, LID> : col_kernel<N, CW, COL_GD_LIN, TGT_F32, P, LID>;
             case COL_EXPECTED: return col_kernel<N, CW, COL_EXPECTED, TGT_F32, P, LID>;
             case COL_FFT_FWD: return col_kernel<N, CW, COL_FFT_FWD, TGT_F32, P, LID>;
             case COL_FFT_INV: return col_kernel<N, CW, COL_FFT_INV, TGT_F32, P, LID>;

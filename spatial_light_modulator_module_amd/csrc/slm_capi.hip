@@ -16,6 +16,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <tuple>
 #include <vector>
 
@@ -59,6 +60,22 @@ int fail(int code, const char* fmt, ...) {
         if (r_ != ncclSuccess) return fail(SLM_ERR_COMM, "%s failed: %s", #expr, ncclGetErrorString(r_)); \
     } while (0)
 
+#define RC(x)                 \
+    do {                      \
+        int rc_ = (x);        \
+        if (rc_) return rc_;  \
+    } while (0)
+
+// Blocking copies go through an explicit stream, never the legacy null stream:
+// slm_gs_multi runs plans from several host threads, and a legacy-stream copy
+// in one thread while another thread captures its plan's graph is an error.
+int copy_sync(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t st) {
+    if (!bytes) return 0;
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, kind, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return 0;
+}
+
 int ensure_device() {
     if (g_device >= 0) {
         HIP_TRY(hipSetDevice(g_device));
@@ -78,8 +95,10 @@ int ensure_device() {
 // [(r - 1) * Ns + j] = exp(-2 pi i j r / (Ns R)), computed in double and
 // stored as float2 (PREC_F32) or double2 (PREC_F64).
 int get_twiddles(int pk, int prec, const void** out) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));  // tables live on the calling thread's current device
     std::lock_guard<std::mutex> lk(g_mu);
-    auto key = std::make_tuple(g_device, pk, prec);
+    auto key = std::make_tuple(dev, pk, prec);
     auto it = g_twiddles.find(key);
     if (it != g_twiddles.end()) {
         *out = it->second;
@@ -110,11 +129,11 @@ int get_twiddles(int pk, int prec, const void** out) {
     void* d = nullptr;
     if (prec == PREC_F64) {
         HIP_TRY(hipMalloc(&d, host.size() * sizeof(double)));
-        HIP_TRY(hipMemcpy(d, host.data(), host.size() * sizeof(double), hipMemcpyHostToDevice));
+        RC(copy_sync(d, host.data(), host.size() * sizeof(double), hipMemcpyHostToDevice, hipStreamPerThread));
     } else {
         std::vector<float> f(host.begin(), host.end());
         HIP_TRY(hipMalloc(&d, f.size() * sizeof(float)));
-        HIP_TRY(hipMemcpy(d, f.data(), f.size() * sizeof(float), hipMemcpyHostToDevice));
+        RC(copy_sync(d, f.data(), f.size() * sizeof(float), hipMemcpyHostToDevice, hipStreamPerThread));
     }
     g_twiddles[key] = d;
     *out = d;
@@ -127,34 +146,59 @@ __global__ void fill_int_kernel(int* p, int n, int v) {
 
 // max(T) and sum(T^2) per hologram in double (np.amax(demanded_output),
 // src/algorithms.py:23; sum(T^2) is the constant term of the error expansion).
-// Stage 1: kTsBlocks workgroups per hologram reduce contiguous chunks.
-constexpr int kTsBlocks = 64;
+// Stage 1: ts_blocks(holo) workgroups per hologram, each thread reducing
+// kTsPerThread consecutive elements from 16-B vector loads (64 MB of a 4096^2
+// float32 target stream at HBM rate: 4096 workgroups, not 64); stage 2 folds
+// a hologram's partials in a fixed order (deterministic).
+constexpr int kTsPerThread = 16;
+constexpr int kTsThreads = 256;
+inline int ts_blocks(long long holo) {
+    return (int)std::max<long long>(1, holo / ((long long)kTsThreads * kTsPerThread));
+}
 template <typename TT>
-__global__ void __launch_bounds__(256) target_stats_partial_kernel(const TT* tgt, long long holo, double* part) {
+__global__ void __launch_bounds__(kTsThreads) target_stats_partial_kernel(const TT* tgt, long long holo, double* part) {
     const int b = blockIdx.y;
-    const long long chunk = (holo + kTsBlocks - 1) / kTsBlocks;
+    const int nblk = gridDim.x;
+    const long long chunk = (holo + nblk - 1) / nblk;
     const long long lo = (long long)blockIdx.x * chunk, hi = min(holo, lo + chunk);
     const TT* p = tgt + (long long)b * holo;
     double mx = 0.0, s2 = 0.0, d = 0.0;
-    for (long long i = lo + threadIdx.x; i < hi; i += 256) {
-        const double v = (double)p[i];
-        mx = fmax(mx, v);
-        s2 += v * v;
+    constexpr int VEC = 16 / sizeof(TT);  // elements per 16-B load
+    const long long vlo = lo / VEC, vhi = hi / VEC;  // holo and chunk are multiples of VEC for supported shapes
+    if ((lo % VEC) == 0 && (hi % VEC) == 0) {
+        for (long long i = vlo + threadIdx.x; i < vhi; i += kTsThreads) {
+            const uint4 q = reinterpret_cast<const uint4*>(p)[i];
+            const TT* e = reinterpret_cast<const TT*>(&q);
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                const double v = (double)e[k];
+                mx = fmax(mx, v);
+                s2 += v * v;
+            }
+        }
+    } else {
+        for (long long i = lo + threadIdx.x; i < hi; i += kTsThreads) {
+            const double v = (double)p[i];
+            mx = fmax(mx, v);
+            s2 += v * v;
+        }
     }
-    block_reduce_stats<256>(mx, s2, d);
+    block_reduce_stats<kTsThreads>(mx, s2, d);
     if (threadIdx.x == 0) {
-        double* o = part + ((long long)b * kTsBlocks + blockIdx.x) * 2;
+        double* o = part + ((long long)b * nblk + blockIdx.x) * 2;
         o[0] = mx;
         o[1] = s2;
     }
 }
-__global__ void __launch_bounds__(64) target_stats_final_kernel(const double* part, double* norm, float* normf,
-                                                                double* sum_t2) {
+__global__ void __launch_bounds__(kTsThreads) target_stats_final_kernel(const double* part, int nblk, double* norm,
+                                                                        float* normf, double* sum_t2) {
     const int b = blockIdx.x;
-    double mx = part[((long long)b * kTsBlocks + threadIdx.x) * 2];
-    double s2 = part[((long long)b * kTsBlocks + threadIdx.x) * 2 + 1];
-    double d = 0.0;
-    block_reduce_stats<64>(mx, s2, d);
+    double mx = 0.0, s2 = 0.0, d = 0.0;
+    for (int k = threadIdx.x; k < nblk; k += kTsThreads) {
+        mx = fmax(mx, part[((long long)b * nblk + k) * 2]);
+        s2 += part[((long long)b * nblk + k) * 2 + 1];
+    }
+    block_reduce_stats<kTsThreads>(mx, s2, d);
     if (threadIdx.x == 0) {
         norm[b] = mx;
         normf[b] = (float)mx;
@@ -185,6 +229,9 @@ int relayout(int plog, const V* in, V* out, long long n, int H, int W, bool to_b
 }
 
 }  // namespace
+
+// GD iteration structures (slm_plan::gd_mode, $SLM_GD_MODE at plan creation)
+enum GdMode : int { GD_AUTO = 0, GD_LIN = 1, GD_FUSED = 2, GD_TWO = 3 };
 
 struct slm_plan {
     int algo = 0, B = 0, H = 0, W = 0, tt = 1, has_ain = 0, max_loops = 0;
@@ -218,7 +265,25 @@ struct slm_plan {
     double* gsync = nullptr;
     long long gsync_len = 0;
     int* gfault = nullptr;
-    int gd_fuse = 1;       // $SLM_GD_FUSE at plan creation (0: two-launch GD column side)
+    int gd_fuse = 1;       // one-launch column side allowed ($SLM_GD_FUSE=0 at creation; cleared by a grid fault)
+    // GD iteration structure ($SLM_GD_MODE=auto|lin|fused|two at plan creation):
+    // GD_AUTO (default): GD_FUSED where the column grid is resident at once
+    //   (float32, unchecked runs), else GD_TWO;
+    // GD_FUSED: one column launch -- forward transform, grid max-barrier,
+    //   gradient and inverse transform on F in registers -- plus the row launch;
+    // GD_TWO: statistics launch + gradient launch that recomputes F;
+    // GD_LIN: column launch stores both inverse-transformed terms (Y, Y2), the
+    //   row launch folds the maxima and combines them (no in-launch wait at all).
+    int gd_mode = GD_AUTO;
+    int skip_wg_plus1 = 0;  // $SLM_GD_FAULT_TEST: fused-path fault injection (tests)
+    int gd_recoveries = 0;  // runs redone on the two-launch path after a grid fault
+    float2* field0 = nullptr;  // GD: host-set initial field (blocked), never overwritten by a run
+    // parameters of the last enqueued run (a grid fault reruns it)
+    int last_loops = 0, last_checked = 0;
+    double last_tol = 0.0;
+    float last_wa = 0.f;
+    float2* y2 = nullptr;   // GD_LIN: column-inverse transform of mask F T
+    double* gmax = nullptr; // GD_LIN: [B][max_loops][nwg] column-workgroup maxima of |F|^2
     double* stats = nullptr;
     int* stop = nullptr;
     double* norm = nullptr;
@@ -228,6 +293,10 @@ struct slm_plan {
     float* lr = nullptr;
     float* gather_buf = nullptr;
     long long gather_elems = 0;
+    double* gather_stats = nullptr;  // slm_plan_gather_stats on the root
+    long long gather_stats_elems = 0;
+    int* gather_stop = nullptr;
+    long long gather_stop_elems = 0;
     bool target_set = false, phase_set = false, field_set = false, lr_set = false;
     // timing state (slm_plan_run_timed)
     bool timing = false;
@@ -246,11 +315,6 @@ struct slm_plan {
 
 namespace {
 
-#define RC(x)                 \
-    do {                      \
-        int rc_ = (x);        \
-        if (rc_) return rc_;  \
-    } while (0)
 
 // Column tile width. With the blocked state layout a 4-column panel is one
 // contiguous run, so a 4-column tile moves whole lines (2-column tiles, which
@@ -382,6 +446,7 @@ RowParams row_params(slm_plan* p) {
     r.phase_in = p->phase_in;
     r.phase_out = p->phase_out;
     r.field = p->field;
+    r.field_src = p->field;
     r.lr = p->lr;
     r.stop_iter = p->stop;
     r.W = p->W;
@@ -416,6 +481,8 @@ ColParams col_params(slm_plan* p) {
 // as the chip holds at once (occupancy query, cached per kernel), never more
 // than there are tiles. $SLM_PERSIST=0 launches one workgroup per tile.
 int tile_grid(const void* fn, int threads, long long tiles, bool persistent, int* grid) {
+    static std::mutex mu;  // slm_gs_multi creates plans from several host threads
+    std::lock_guard<std::mutex> lk(mu);
     static std::map<const void*, int> resident;
     static int cus = 0, persist = -1;
     if (persist < 0) {
@@ -464,6 +531,16 @@ int launch_col(slm_plan* p, int mode, const ColParams& cp, int cls) {
     RC(tile_grid((const void*)fn, p->col_threads, (long long)p->nwg * p->B,
                   tile_persistent(p->prec, kPlans[p->col_key].e), &grid));
     return launch(p, cls, fn, dim3(grid), dim3(p->col_threads), c);
+}
+
+// expected output |C|^2 (src/algorithms.py:36): the column kernel writes it in
+// layout Y into the free Y buffer (every reader of Y precedes this on the
+// stream), then one relayout to the row-major e_out
+int launch_expected(slm_plan* p, ColParams cp) {
+    cp.e_blk = reinterpret_cast<float*>(p->y);
+    RC(launch_col(p, COL_EXPECTED, cp, SLM_KERNEL_OTHER));
+    return relayout(layout_y_log2(p->lid), (const float*)p->y, p->e_out, (long long)p->B * p->holo, p->H, p->W,
+                    false, p->stream);
 }
 
 StatsParams stats_params(slm_plan* p, double tol) {
@@ -523,7 +600,7 @@ int enqueue_gs(slm_plan* p, int loops, double tol, int checked) {
     RC(launch_row(p, ROW_GS_PHASE, rp, SLM_KERNEL_OTHER));
     cp.in = p->xa;
     cp.in_alt = p->xa;
-    RC(launch_col(p, COL_EXPECTED, cp, SLM_KERNEL_OTHER));
+    RC(launch_expected(p, cp));
     return 0;
 }
 
@@ -534,6 +611,8 @@ int enqueue_gs(slm_plan* p, int loops, double tol, int checked) {
 // the gradient pass run as two launches. $SLM_GD_FUSE=0 forces two launches.
 ColFn gd_fused_fn(slm_plan* p, int checked) {
     if (!p->gd_fuse || !p->gsync || checked || tile_persistent(p->prec, kPlans[p->col_key].e)) return nullptr;
+    if (p->gd_mode != GD_AUTO && p->gd_mode != GD_FUSED) return nullptr;
+    if (2LL * p->B * p->max_loops * (1 + p->nwg) > INT_MAX) return nullptr;  // slot area: two launches instead
     ColFn fn = col_fn(p->col_key, p->cw, COL_GD_FUSED, p->tt, p->prec, p->lid);
     if (!fn) return nullptr;
     int dev = 0, cus = 0, per_cu = 0;
@@ -554,6 +633,7 @@ int enqueue_gd(slm_plan* p, int loops, double tol, int checked, float wa) {
     // or the "fourier" guess a_in exp(i angle(ifft2(sqrt T))).
     if (p->field_set) {
         rp.out = p->xa;
+        rp.field_src = p->field0;
         RC(launch_row(p, ROW_GD_INIT_FIELD, rp, SLM_KERNEL_OTHER));
     } else {
         cp.out = p->y;
@@ -562,23 +642,43 @@ int enqueue_gd(slm_plan* p, int loops, double tol, int checked, float wa) {
         rp.out = p->xa;
         RC(launch_row(p, ROW_GD_INIT_Y, rp, SLM_KERNEL_OTHER));
     }
-    const bool fused = gd_fused_fn(p, checked) != nullptr;
+    const bool lin = p->gd_mode == GD_LIN;
+    const bool fused = !lin && gd_fused_fn(p, checked) != nullptr;
     if (fused) {
         cp.gresult = p->gsync;
         cp.gslots = p->gsync + (long long)p->B * p->max_loops;
         cp.fault = p->gfault;
+        cp.skip_wg_plus1 = p->skip_wg_plus1;
         // every result and slot word to kUnset (all bits set) before the run
+        // (gd_fused_fn keeps the slot area within INT_MAX words)
         const long long words = 2LL * p->B * p->max_loops * (1 + p->nwg);
-        if (words > INT_MAX) return fail(SLM_ERR_ARG, "grid barrier area too large");
         RC(launch(p, SLM_KERNEL_OTHER, fill_int_kernel, dim3((int)std::min<long long>(65535, (words + 255) / 256)),
                   dim3(256), (int*)p->gsync, (int)words, -1));
     }
     for (int i = 0; i < loops; ++i) {
         float2* xi = (i & 1) ? p->xb : p->xa;
         float2* xn = (i & 1) ? p->xa : p->xb;
+        // iteration 0 reads a host-set field from field0 (kept intact for reruns)
+        rp.field_src = (i == 0 && p->field_set) ? p->field0 : p->field;
         cp.in = xi;
         cp.iter = i;
         cp.out = p->y;
+        if (lin) {
+            cp.out2 = p->y2;
+            cp.gmax = p->gmax;
+            RC(launch_col(p, COL_GD_LIN, cp, SLM_KERNEL_COL_MAIN));
+            if (checked) RC(launch_finalize(p, tol, i));
+            rp.in = p->y;
+            rp.in2 = p->y2;
+            rp.gmax = p->gmax;
+            rp.norm = p->normf;
+            rp.nwg_col = p->nwg;
+            rp.max_loops = p->max_loops;
+            rp.out = xn;
+            rp.iter = i;
+            RC(launch_row(p, ROW_GD_LIN, rp, SLM_KERNEL_ROW_MAIN));
+            continue;
+        }
         if (fused) {
             RC(launch_col(p, COL_GD_FUSED, cp, SLM_KERNEL_COL_MAIN));
         } else {
@@ -601,20 +701,33 @@ int enqueue_gd(slm_plan* p, int loops, double tol, int checked, float wa) {
     }
     cp.in = p->xa;
     cp.in_alt = p->xb;
-    RC(launch_col(p, COL_EXPECTED, cp, SLM_KERNEL_OTHER));
+    RC(launch_expected(p, cp));
     return 0;
 }
 
-// A grid barrier of COL_GD_FUSED that gave up waiting (kernels.hpp,
-// grid_arrive_wait) leaves a fault flag: the run's results are invalid.
-int check_grid_fault(slm_plan* p) {
+// A grid wait of COL_GD_FUSED that gave up (kernels.hpp, wait_set) leaves a
+// fault flag: that run's results are invalid. Read it after the stream has
+// drained; on a fault the plan gives up its one-launch column side for good
+// (its workgroups were not co-resident: other work shares the device) and
+// redoes the same run on the two-launch path in-process (the run's inputs --
+// target, field0, learning rates -- are untouched by a run). *faulted tells
+// the caller that the stream now holds the rerun.
+int recover_grid_fault(slm_plan* p, bool* faulted) {
+    *faulted = false;
     if (!p->gfault) return 0;
     int f = 0;
-    int* flag = p->gfault;
-    HIP_TRY(hipMemcpy(&f, flag, sizeof(int), hipMemcpyDeviceToHost));
+    RC(copy_sync(&f, p->gfault, sizeof(int), hipMemcpyDeviceToHost, p->stream));
     if (!f) return 0;
-    HIP_TRY(hipMemset(flag, 0, sizeof(int)));
-    return fail(SLM_ERR_HIP, "GD grid barrier timed out (workgroups not co-resident); rerun with SLM_GD_FUSE=0");
+    HIP_TRY(hipMemsetAsync(p->gfault, 0, sizeof(int), p->stream));
+    HIP_TRY(hipStreamSynchronize(p->stream));
+    *faulted = true;
+    p->gd_fuse = 0;
+    p->gd_recoveries += 1;
+    if (p->gexec) {  // the captured run holds the fused kernel
+        HIP_TRY(hipGraphExecDestroy(p->gexec));
+        p->gexec = nullptr;
+    }
+    return 0;
 }
 
 int enqueue_run(slm_plan* p, int loops, double tol, int checked, float wa) {
@@ -639,8 +752,8 @@ void free_plan(slm_plan* p) {
                       (void*)p->phase_in, (void*)p->phase_out, (void*)p->e_out, (void*)p->partials,
                       (void*)p->stats, (void*)p->stop, (void*)p->norm, (void*)p->normf, (void*)p->sum_t2,
                       (void*)p->ts_part, (void*)p->lr, (void*)p->gsync, (void*)p->gfault, (void*)p->gather_buf,
-                      (void*)p->trace_col,
-                      (void*)p->trace_row})
+                      (void*)p->gather_stats, (void*)p->gather_stop, (void*)p->y2, (void*)p->gmax,
+                      (void*)p->field0, (void*)p->trace_col, (void*)p->trace_row})
         if (ptr) (void)hipFree(ptr);
     for (auto& e : p->ev_pool) {
         (void)hipEventDestroy(e.first);
@@ -686,8 +799,26 @@ const char* slm_version(void) { return "libslm_hip 0.1 (gfx950)"; }
 
 int slm_supported_length(int n) { return plan_index(n) >= 0 ? 1 : 0; }
 
+}  // extern "C"
+
+namespace {
+int plan_create_on(int device, int algo, int batch, int height, int width, int tgt_type, int has_ain,
+                   int max_loops, slm_plan** out);
+}
+
+extern "C" {
+
 int slm_plan_create(int algo, int batch, int height, int width, int tgt_type, int has_ain, int max_loops,
                     slm_plan** out) {
+    RC(ensure_device());
+    return plan_create_on(g_device, algo, batch, height, width, tgt_type, has_ain, max_loops, out);
+}
+
+}  // extern "C"
+
+namespace {
+int plan_create_on(int device, int algo, int batch, int height, int width, int tgt_type, int has_ain,
+                   int max_loops, slm_plan** out) {
     if (!out) return fail(SLM_ERR_ARG, "null output pointer");
     *out = nullptr;
     if (algo != SLM_ALGO_GS && algo != SLM_ALGO_GD) return fail(SLM_ERR_ARG, "unknown algorithm %d", algo);
@@ -698,7 +829,7 @@ int slm_plan_create(int algo, int batch, int height, int width, int tgt_type, in
                     "image shape %dx%d unsupported: each side must be one of 64, 128, 256, 512, 768, 1024, "
                     "2048, 4096",
                     height, width);
-    RC(ensure_device());
+    HIP_TRY(hipSetDevice(device));
     slm_plan* p = new slm_plan();
     p->algo = algo;
     p->B = batch;
@@ -707,12 +838,20 @@ int slm_plan_create(int algo, int batch, int height, int width, int tgt_type, in
     p->tt = tgt_type;
     p->has_ain = has_ain ? 1 : 0;
     p->max_loops = max_loops;
-    p->device = g_device;
+    p->device = device;
     p->holo = (long long)height * width;
     p->wt_col = height >= 2048 ? 0 : 1;
     p->wt_row = ((long long)batch * p->holo >= (32LL << 20) || width >= 4096) ? 0 : 1;
     if (const char* e = std::getenv("SLM_WT")) p->wt_col = p->wt_row = std::atoi(e) != 0;
     if (const char* e = std::getenv("SLM_GD_FUSE")) p->gd_fuse = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SLM_GD_MODE"))
+        p->gd_mode = !std::strcmp(e, "fused") ? GD_FUSED
+                     : !std::strcmp(e, "two") ? GD_TWO
+                     : !std::strcmp(e, "lin") ? GD_LIN
+                                              : GD_AUTO;
+    if (!p->gd_fuse && p->gd_mode != GD_LIN) p->gd_mode = GD_TWO;
+    if (p->gd_mode == GD_TWO || p->gd_mode == GD_LIN) p->gd_fuse = 0;
+    if (const char* e = std::getenv("SLM_GD_FAULT_TEST")) p->skip_wg_plus1 = std::atoi(e);
     if (const char* e = std::getenv("SLM_PRECISION")) p->prec = (std::strcmp(e, "f64") == 0) ? PREC_F64 : PREC_F32;
     // buffers indexed by column panel / row group hold the finer tiling of both precisions
     int max_nwg = 0, min_rpw = INT_MAX;
@@ -750,13 +889,19 @@ int slm_plan_create(int algo, int batch, int height, int width, int tgt_type, in
     if (algo == SLM_ALGO_GD) {
         RC(alloc((void**)&p->xb, n * sizeof(float2)));
         RC(alloc((void**)&p->field, n * sizeof(float2)));
+        RC(alloc((void**)&p->field0, n * sizeof(float2)));
         RC(alloc((void**)&p->lr, (size_t)max_loops * sizeof(float)));
+        if (p->gd_mode == GD_LIN) {
+            RC(alloc((void**)&p->y2, n * sizeof(float2)));
+            RC(alloc((void**)&p->gmax, (size_t)batch * max_loops * max_nwg * sizeof(double)));
+        }
         // the one-launch column side needs the whole grid resident: never beyond 8192 workgroups
-        if ((long long)batch * max_nwg <= 8192) {
+        if ((p->gd_mode == GD_FUSED || p->gd_mode == GD_AUTO) && (long long)batch * max_nwg <= 8192) {
             p->gsync_len = (long long)batch * max_loops * (1 + max_nwg);
             RC(alloc((void**)&p->gsync, (size_t)p->gsync_len * sizeof(double)));
             RC(alloc((void**)&p->gfault, sizeof(int)));
-            HIP_TRY(hipMemset(p->gfault, 0, sizeof(int)));
+            HIP_TRY(hipMemsetAsync(p->gfault, 0, sizeof(int), p->stream));
+    HIP_TRY(hipStreamSynchronize(p->stream));
         }
     }
     RC(alloc(&p->tgt, n * tb));
@@ -769,7 +914,7 @@ int slm_plan_create(int algo, int batch, int height, int width, int tgt_type, in
     RC(alloc((void**)&p->norm, (size_t)batch * sizeof(double)));
     RC(alloc((void**)&p->normf, (size_t)batch * sizeof(float)));
     RC(alloc((void**)&p->sum_t2, (size_t)batch * sizeof(double)));
-    RC(alloc((void**)&p->ts_part, (size_t)batch * kTsBlocks * 2 * sizeof(double)));
+    RC(alloc((void**)&p->ts_part, (size_t)batch * ts_blocks(p->holo) * 2 * sizeof(double)));
     if (const char* e = std::getenv("SLM_TRACE_BUF"); e && std::atoi(e)) {
         RC(alloc((void**)&p->trace_col, (size_t)batch * max_nwg * kTraceSlots * sizeof(unsigned long long)));
         RC(alloc((void**)&p->trace_row, (size_t)batch * (height / min_rpw) * kTraceSlots * sizeof(unsigned long long)));
@@ -778,6 +923,10 @@ int slm_plan_create(int algo, int batch, int height, int width, int tgt_type, in
     return 0;
 }
 
+}  // namespace
+
+extern "C" {
+
 int slm_plan_read_trace(slm_plan* p, int kernel_class, unsigned long long* out) {
     if (!p || !out) return fail(SLM_ERR_ARG, "null argument");
     unsigned long long* src = kernel_class == SLM_KERNEL_COL_MAIN ? p->trace_col
@@ -785,7 +934,7 @@ int slm_plan_read_trace(slm_plan* p, int kernel_class, unsigned long long* out) 
     if (!src) return fail(SLM_ERR_STATE, "no trace buffer (set SLM_TRACE_BUF=1 before creating the plan)");
     const long long n = (long long)p->B * (kernel_class == SLM_KERNEL_COL_MAIN ? p->nwg : p->H / p->rpw) * kTraceSlots;
     HIP_TRY(hipStreamSynchronize(p->stream));
-    HIP_TRY(hipMemcpy(out, src, n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    RC(copy_sync(out, src, n * sizeof(unsigned long long), hipMemcpyDeviceToHost, p->stream));
     return 0;
 }
 
@@ -801,17 +950,18 @@ int slm_plan_set_target(slm_plan* p, const void* tgt) {
     const size_t tb = p->tt == SLM_TGT_U8 ? 1 : 4;
     void* stage = p->e_out;  // n floats >= n target elements of either type
     HIP_TRY(hipMemcpyAsync(stage, tgt, (size_t)n * tb, hipMemcpyHostToDevice, p->stream));
+    const int nblk = ts_blocks(p->holo);
     if (p->tt == SLM_TGT_U8) {
-        hipLaunchKernelGGL(target_stats_partial_kernel<uint8_t>, dim3(kTsBlocks, p->B), dim3(256), 0, p->stream,
+        hipLaunchKernelGGL(target_stats_partial_kernel<uint8_t>, dim3(nblk, p->B), dim3(kTsThreads), 0, p->stream,
                            (const uint8_t*)stage, p->holo, p->ts_part);
         RC(relayout(layout_x_log2(p->lid), (const uint8_t*)stage, (uint8_t*)p->tgt, n, p->H, p->W, true, p->stream));
     } else {
-        hipLaunchKernelGGL(target_stats_partial_kernel<float>, dim3(kTsBlocks, p->B), dim3(256), 0, p->stream,
+        hipLaunchKernelGGL(target_stats_partial_kernel<float>, dim3(nblk, p->B), dim3(kTsThreads), 0, p->stream,
                            (const float*)stage, p->holo, p->ts_part);
         RC(relayout(layout_x_log2(p->lid), (const float*)stage, (float*)p->tgt, n, p->H, p->W, true, p->stream));
     }
-    hipLaunchKernelGGL(target_stats_final_kernel, dim3(p->B), dim3(kTsBlocks), 0, p->stream, p->ts_part, p->norm,
-                       p->normf, p->sum_t2);
+    hipLaunchKernelGGL(target_stats_final_kernel, dim3(p->B), dim3(kTsThreads), 0, p->stream, p->ts_part, nblk,
+                       p->norm, p->normf, p->sum_t2);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(p->stream));
     p->target_set = true;
@@ -867,7 +1017,7 @@ int slm_plan_set_field(slm_plan* p, const float* field) {
     }
     const long long n = (long long)p->B * p->holo;
     HIP_TRY(hipMemcpyAsync(p->y, field, (size_t)n * sizeof(float2), hipMemcpyHostToDevice, p->stream));
-    RC(relayout(layout_y_log2(p->lid), (const float2*)p->y, p->field, n, p->H, p->W, true, p->stream));
+    RC(relayout(layout_y_log2(p->lid), (const float2*)p->y, p->field0, n, p->H, p->W, true, p->stream));
     HIP_TRY(hipStreamSynchronize(p->stream));
     p->field_set = true;
     return 0;
@@ -884,7 +1034,13 @@ int slm_plan_set_lr(slm_plan* p, const float* lr) {
 }
 
 int slm_plan_run(slm_plan* p, int loops, double tol, int checked, float wa) {
-    if (p) p->timing = false;
+    if (p) {
+        p->timing = false;
+        p->last_loops = loops;
+        p->last_tol = tol;
+        p->last_checked = checked;
+        p->last_wa = wa;
+    }
     static const bool use_graph = [] {
         const char* e = std::getenv("SLM_GRAPH");
         return !e || std::atoi(e) != 0;
@@ -930,7 +1086,9 @@ int slm_plan_run_timed(slm_plan* p, int loops, double tol, int checked, float wa
     p->timing = false;
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(p->stream));
-    RC(check_grid_fault(p));
+    bool faulted = false;
+    RC(recover_grid_fault(p, &faulted));
+    if (faulted) return slm_plan_run_timed(p, loops, tol, checked, wa, us, counts);  // now on two launches
     for (int k = 0; k < SLM_NUM_KERNEL_CLASSES; ++k) {
         if (us) us[k] = 0.0;
         if (counts) counts[k] = 0;
@@ -949,23 +1107,29 @@ int slm_plan_sync(slm_plan* p) {
     if (!p) return fail(SLM_ERR_ARG, "null plan");
     HIP_TRY(hipSetDevice(p->device));
     HIP_TRY(hipStreamSynchronize(p->stream));
-    return check_grid_fault(p);
+    bool faulted = false;
+    RC(recover_grid_fault(p, &faulted));
+    if (faulted) {  // the last run again, on the two-launch column side (cannot fault)
+        RC(slm_plan_run(p, p->last_loops, p->last_tol, p->last_checked, p->last_wa));
+        HIP_TRY(hipStreamSynchronize(p->stream));
+    }
+    return 0;
 }
+
+int slm_plan_gd_recoveries(slm_plan* p) { return p ? p->gd_recoveries : -1; }
 
 int slm_plan_read(slm_plan* p, float* phase, float* expected, double* stats, int* iters) {
     if (!p) return fail(SLM_ERR_ARG, "null plan");
-    HIP_TRY(hipSetDevice(p->device));
-    HIP_TRY(hipStreamSynchronize(p->stream));
-    RC(check_grid_fault(p));
+    RC(slm_plan_sync(p));
     const size_t n = (size_t)p->B * p->holo;
-    if (phase) HIP_TRY(hipMemcpy(phase, p->phase_out, n * sizeof(float), hipMemcpyDeviceToHost));
-    if (expected) HIP_TRY(hipMemcpy(expected, p->e_out, n * sizeof(float), hipMemcpyDeviceToHost));
+    if (phase) RC(copy_sync(phase, p->phase_out, n * sizeof(float), hipMemcpyDeviceToHost, p->stream));
+    if (expected) RC(copy_sync(expected, p->e_out, n * sizeof(float), hipMemcpyDeviceToHost, p->stream));
     if (stats)
-        HIP_TRY(hipMemcpy(stats, p->stats, (size_t)p->B * p->max_loops * 4 * sizeof(double),
-                          hipMemcpyDeviceToHost));
+        RC(copy_sync(stats, p->stats, (size_t)p->B * p->max_loops * 4 * sizeof(double),
+                          hipMemcpyDeviceToHost, p->stream));
     if (iters) {
         std::vector<int> st(p->B);
-        HIP_TRY(hipMemcpy(st.data(), p->stop, (size_t)p->B * sizeof(int), hipMemcpyDeviceToHost));
+        RC(copy_sync(st.data(), p->stop, (size_t)p->B * sizeof(int), hipMemcpyDeviceToHost, p->stream));
         for (int b = 0; b < p->B; ++b) iters[b] = st[b] == INT_MAX ? -1 : st[b] + 1;  // -1: ran all loops
     }
     return 0;
@@ -975,8 +1139,8 @@ int slm_plan_read_target_stats(slm_plan* p, double* norm, double* sum_t2) {
     if (!p) return fail(SLM_ERR_ARG, "null plan");
     HIP_TRY(hipSetDevice(p->device));
     HIP_TRY(hipStreamSynchronize(p->stream));
-    if (norm) HIP_TRY(hipMemcpy(norm, p->norm, (size_t)p->B * sizeof(double), hipMemcpyDeviceToHost));
-    if (sum_t2) HIP_TRY(hipMemcpy(sum_t2, p->sum_t2, (size_t)p->B * sizeof(double), hipMemcpyDeviceToHost));
+    if (norm) RC(copy_sync(norm, p->norm, (size_t)p->B * sizeof(double), hipMemcpyDeviceToHost, p->stream));
+    if (sum_t2) RC(copy_sync(sum_t2, p->sum_t2, (size_t)p->B * sizeof(double), hipMemcpyDeviceToHost, p->stream));
     return 0;
 }
 
@@ -998,10 +1162,11 @@ long long slm_plan_kernel_bytes(slm_plan* p, int cls) {
     const long long px = (long long)p->B * p->holo;
     const long long tb = p->tt == SLM_TGT_U8 ? 1 : 4;
     const long long ab = p->has_ain ? 4 : 0;
+    const bool lin = p->algo == SLM_ALGO_GD && p->gd_mode == GD_LIN;  // + Y2 out (column) / in (row)
     switch (cls) {
-        case SLM_KERNEL_COL_MAIN: return px * (8 + tb + 8);       // X (GD: F) in, T in, Y out
+        case SLM_KERNEL_COL_MAIN: return px * (8 + tb + 8 + (lin ? 8 : 0));  // X (GD: F) in, T in, Y out
         case SLM_KERNEL_ROW_MAIN:                                 // Y in, X out (+ a_in) (+ field r/w for GD)
-            return px * (16 + ab + (p->algo == SLM_ALGO_GD ? 16 : 0));
+            return px * (16 + ab + (p->algo == SLM_ALGO_GD ? 16 : 0) + (lin ? 8 : 0));
         case SLM_KERNEL_GD_STATS: return px * (8 + tb);           // X in, T in
         default: return 0;
     }
@@ -1056,6 +1221,61 @@ int slm_gd(const void* tgt, int tgt_type, const float* ain, int batch, int heigh
     return rc;
 }
 
+int slm_gs_multi(int n_gpus, const int* devices, const void* tgt, int tgt_type, const float* ain, int batch,
+                 int height, int width, int max_loops, double tol, const float* init_phase, float* out_phase,
+                 float* out_expected, double* out_stats, int* out_iters) {
+    if (n_gpus < 1) return fail(SLM_ERR_ARG, "n_gpus must be >= 1");
+    if (!tgt || batch < 1) return fail(SLM_ERR_ARG, "need a target batch");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return fail(SLM_ERR_HIP, "no HIP device available; libslm_hip has no CPU path");
+    std::vector<int> dev(n_gpus);
+    for (int r = 0; r < n_gpus; ++r) {
+        dev[r] = devices ? devices[r] : r;
+        if (dev[r] < 0 || dev[r] >= ndev) return fail(SLM_ERR_ARG, "shard %d: device %d outside [0, %d)", r, dev[r], ndev);
+    }
+    // contiguous shards in batch order, the first batch % n_gpus one larger
+    // (parallel.shard_counts; the same arithmetic as slm_gather_layout)
+    std::vector<int> counts(n_gpus);
+    for (int r = 0; r < n_gpus; ++r) counts[r] = batch / n_gpus + (r < batch % n_gpus ? 1 : 0);
+    std::vector<long long> off(n_gpus + 1);
+    RC(slm_gather_layout(n_gpus, counts.data(), 1, off.data()));
+    const long long holo = (long long)height * width;
+    const size_t tb = tgt_type == SLM_TGT_U8 ? 1 : 4;
+    std::vector<int> rcs(n_gpus, 0);
+    std::vector<std::string> errs(n_gpus);
+    auto shard = [&](int r) {
+        if (!counts[r]) return;
+        const long long h0 = off[r];
+        slm_plan* p = nullptr;
+        int rc = plan_create_on(dev[r], SLM_ALGO_GS, counts[r], height, width, tgt_type, ain != nullptr, max_loops,
+                                &p);
+        if (!rc) rc = slm_plan_set_target(p, static_cast<const char*>(tgt) + (size_t)h0 * holo * tb);
+        if (!rc && ain) rc = slm_plan_set_ain(p, ain);
+        if (!rc && init_phase) rc = slm_plan_set_phase(p, init_phase + h0 * holo);
+        if (!rc) rc = slm_plan_run(p, max_loops, tol, tol > 0.0 ? 1 : 0, 0.f);
+        // each shard lands in its own slice of the caller's arrays over its GPU's own link
+        if (!rc)
+            rc = slm_plan_read(p, out_phase ? out_phase + h0 * holo : nullptr,
+                               out_expected ? out_expected + h0 * holo : nullptr,
+                               out_stats ? out_stats + h0 * (long long)max_loops * 4 : nullptr,
+                               out_iters ? out_iters + h0 : nullptr);
+        if (rc) errs[r] = g_err;  // thread-local message of this shard's thread
+        free_plan(p);
+        rcs[r] = rc;
+    };
+    if (n_gpus == 1) {
+        shard(0);
+    } else {
+        std::vector<std::thread> th;
+        for (int r = 0; r < n_gpus; ++r) th.emplace_back(shard, r);
+        for (auto& t : th) t.join();
+    }
+    for (int r = 0; r < n_gpus; ++r)
+        if (rcs[r]) return fail(rcs[r], "shard %d (device %d): %s", r, dev[r], errs[r].c_str());
+    return 0;
+}
+
 int slm_fft2(const float* in, float* out, int batch, int height, int width, int inverse) {
     if (!in || !out) return fail(SLM_ERR_ARG, "null argument");
     slm_plan* p = nullptr;
@@ -1081,7 +1301,8 @@ int slm_fft2(const float* in, float* out, int batch, int height, int width, int 
     if (!rc) rc = relayout(layout_y_log2(p->lid), (const float2*)p->xa, p->y, n, height, width, false, p->stream);  // col-pass output
     if (!rc) {
         e = hipStreamSynchronize(p->stream);
-        if (e == hipSuccess) e = hipMemcpy(out, p->y, bytes, hipMemcpyDeviceToHost);
+        if (e == hipSuccess) e = hipMemcpyAsync(out, p->y, bytes, hipMemcpyDeviceToHost, p->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
         if (e != hipSuccess) rc = fail(SLM_ERR_HIP, "fft2 failed: %s", hipGetErrorString(e));
     }
     free_plan(p);
@@ -1104,7 +1325,7 @@ int slm_fft2_intensity(const float* phase, int batch, int height, int width, flo
         cp.loops = 1;
         cp.in = p->xa;
         cp.in_alt = p->xa;
-        if (!rc) rc = launch_col(p, COL_EXPECTED, cp, SLM_KERNEL_OTHER);
+        if (!rc) rc = launch_expected(p, cp);
     }
     if (!rc) rc = slm_plan_read(p, nullptr, intensity_out, nullptr, nullptr);
     free_plan(p);
@@ -1119,7 +1340,7 @@ int slm_plan_read_field(slm_plan* p, float* field) {
     // p->y is scratch between runs (every run rewrites it before reading it)
     RC(relayout(layout_y_log2(p->lid), (const float2*)p->field, p->y, n, p->H, p->W, false, p->stream));
     HIP_TRY(hipStreamSynchronize(p->stream));
-    HIP_TRY(hipMemcpy(field, p->y, (size_t)n * sizeof(float2), hipMemcpyDeviceToHost));
+    RC(copy_sync(field, p->y, (size_t)n * sizeof(float2), hipMemcpyDeviceToHost, p->stream));
     return 0;
 }
 
@@ -1154,42 +1375,92 @@ int slm_comm_destroy(void) {
     return 0;
 }
 
-int slm_plan_gather_phase(slm_plan* p, const int* counts, int root, float* host_out) {
+int slm_gather_layout(int nranks, const int* counts, long long per_item, long long* offsets) {
+    if (nranks < 1 || !counts || !offsets || per_item < 0) return fail(SLM_ERR_ARG, "bad gather layout arguments");
+    long long off = 0;
+    for (int r = 0; r < nranks; ++r) {
+        if (counts[r] < 0) return fail(SLM_ERR_ARG, "counts[%d] = %d is negative", r, counts[r]);
+        offsets[r] = off;
+        off += (long long)counts[r] * per_item;
+    }
+    offsets[nranks] = off;
+    return 0;
+}
+
+}  // extern "C"
+
+namespace {
+
+// Gather one per-hologram slab of every rank to `root` (rank order): `src`
+// holds this rank's counts[me] x per_item elements of `elem` bytes (RCCL type
+// `dt`); on root the concatenation lands in *dev_buf (grown as needed) and,
+// if host_out, on the host. Grouped ncclSend / ncclRecv on the plan stream
+// (one xGMI hop per peer), synchronised before returning.
+int gather_slab(slm_plan* p, const void* src, long long per_item, size_t elem, ncclDataType_t dt, const int* counts,
+                int root, void** dev_buf, long long* dev_cap, void* host_out) {
     if (!p || !counts) return fail(SLM_ERR_ARG, "null argument");
     HIP_TRY(hipSetDevice(p->device));
     const int n = g_comm ? g_comm_size : 1;
     const int me = g_comm ? g_comm_rank : 0;
+    if (root < 0 || root >= n) return fail(SLM_ERR_ARG, "root %d outside [0, %d)", root, n);
     if (counts[me] != p->B) return fail(SLM_ERR_ARG, "counts[%d]=%d but the plan holds %d", me, counts[me], p->B);
-    long long total = 0;
-    for (int r = 0; r < n; ++r) total += counts[r];
+    std::vector<long long> off(n + 1);
+    RC(slm_gather_layout(n, counts, per_item, off.data()));
     if (me == root) {
-        const long long elems = total * p->holo;
-        if (p->gather_elems < elems) {
-            if (p->gather_buf) HIP_TRY(hipFree(p->gather_buf));
-            HIP_TRY(hipMalloc((void**)&p->gather_buf, elems * sizeof(float)));
-            p->gather_elems = elems;
+        const long long elems = off[n];
+        if (*dev_cap < elems) {
+            if (*dev_buf) HIP_TRY(hipFree(*dev_buf));
+            *dev_buf = nullptr;
+            *dev_cap = 0;
+            HIP_TRY(hipMalloc(dev_buf, std::max<long long>(elems, 1) * elem));
+            *dev_cap = elems;
         }
-        long long off = 0;
+        char* dst = static_cast<char*>(*dev_buf);
         if (n > 1) NCCL_TRY(ncclGroupStart());
         for (int r = 0; r < n; ++r) {
-            const size_t cnt = (size_t)counts[r] * p->holo;
+            const size_t cnt = (size_t)(off[r + 1] - off[r]);
+            if (!cnt) continue;
             if (r == me) {
-                HIP_TRY(hipMemcpyAsync(p->gather_buf + off, p->phase_out, cnt * sizeof(float),
-                                       hipMemcpyDeviceToDevice, p->stream));
-            } else if (cnt) {
-                NCCL_TRY(ncclRecv(p->gather_buf + off, cnt, ncclFloat32, r, g_comm, p->stream));
+                HIP_TRY(hipMemcpyAsync(dst + off[r] * elem, src, cnt * elem, hipMemcpyDeviceToDevice, p->stream));
+            } else {
+                NCCL_TRY(ncclRecv(dst + off[r] * elem, cnt, dt, r, g_comm, p->stream));
             }
-            off += (long long)counts[r] * p->holo;
         }
         if (n > 1) NCCL_TRY(ncclGroupEnd());
         HIP_TRY(hipStreamSynchronize(p->stream));
-        if (host_out)
-            HIP_TRY(hipMemcpy(host_out, p->gather_buf, (size_t)elems * sizeof(float), hipMemcpyDeviceToHost));
+        if (host_out && elems) RC(copy_sync(host_out, dst, (size_t)elems * elem, hipMemcpyDeviceToHost, p->stream));
     } else {
         if (!g_comm) return fail(SLM_ERR_COMM, "no communicator");
-        if (p->B)
-            NCCL_TRY(ncclSend(p->phase_out, (size_t)p->B * p->holo, ncclFloat32, root, g_comm, p->stream));
+        if (p->B) NCCL_TRY(ncclSend(src, (size_t)p->B * per_item, dt, root, g_comm, p->stream));
         HIP_TRY(hipStreamSynchronize(p->stream));
+    }
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int slm_plan_gather_phase(slm_plan* p, const int* counts, int root, float* host_out) {
+    if (!p) return fail(SLM_ERR_ARG, "null plan");
+    return gather_slab(p, p->phase_out, p->holo, sizeof(float), ncclFloat32, counts, root, (void**)&p->gather_buf,
+                       &p->gather_elems, host_out);
+}
+
+int slm_plan_gather_stats(slm_plan* p, const int* counts, int root, double* stats_out, int* iters_out) {
+    if (!p) return fail(SLM_ERR_ARG, "null plan");
+    // per hologram: [max_loops][4] doubles (max E, sum E^2, sum E T, error), then the stop index
+    RC(gather_slab(p, p->stats, (long long)p->max_loops * 4, sizeof(double), ncclFloat64, counts, root,
+                   (void**)&p->gather_stats, &p->gather_stats_elems, stats_out));
+    RC(gather_slab(p, p->stop, 1, sizeof(int), ncclInt32, counts, root, (void**)&p->gather_stop,
+                   &p->gather_stop_elems, iters_out));
+    if (iters_out) {  // the stop index -> iterations executed, as slm_plan_read reports it
+        const int n = g_comm ? g_comm_size : 1;
+        if ((g_comm ? g_comm_rank : 0) == root) {
+            long long total = 0;
+            for (int r = 0; r < n; ++r) total += counts[r];
+            for (long long k = 0; k < total; ++k) iters_out[k] = iters_out[k] == INT_MAX ? -1 : iters_out[k] + 1;
+        }
     }
     return 0;
 }

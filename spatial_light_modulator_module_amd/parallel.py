@@ -16,6 +16,7 @@ keeps MASTER_PORT for its own store).
 """
 from __future__ import annotations
 
+import hmac
 import os
 import pickle
 import socket
@@ -63,8 +64,23 @@ def free_port(addr: str = "127.0.0.1") -> int:
         return s.getsockname()[1]
 
 
+# Largest control-plane message a rank accepts (error lists, unique ids and
+# timings are far smaller); a longer length prefix is refused, never allocated.
+MAX_MESSAGE = 64 << 20
+_HELLO_MAGIC = b"SLMh"
+_MAX_TOKEN = 256
+
+
+def job_token() -> bytes:
+    """Shared secret of one job's ranks: $SLM_JOB_TOKEN (bench.py's own
+    launcher draws a random one), else torchrun's per-job run id."""
+    return (os.environ.get("SLM_JOB_TOKEN") or os.environ.get("TORCHELASTIC_RUN_ID") or "").encode()[:_MAX_TOKEN]
+
+
 def _send(sock, obj) -> None:
     data = pickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL)
+    if len(data) > MAX_MESSAGE:
+        raise ValueError(f"control-plane message of {len(data)} bytes exceeds {MAX_MESSAGE}")
     sock.sendall(struct.pack("!Q", len(data)) + data)
 
 
@@ -80,15 +96,38 @@ def _recv_exact(sock, n: int) -> bytes:
 
 def _recv(sock):
     (n,) = struct.unpack("!Q", _recv_exact(sock, 8))
-    return pickle.loads(_recv_exact(sock, n))  # peers are this job's own ranks
+    if n > MAX_MESSAGE:
+        raise ConnectionError(f"control-plane message of {n} bytes exceeds {MAX_MESSAGE}")
+    return pickle.loads(_recv_exact(sock, n))  # only peers that passed the hello check reach here
+
+
+def _send_hello(sock, rank: int, token: bytes) -> None:
+    sock.sendall(_HELLO_MAGIC + struct.pack("!IH", rank, len(token)) + token)
+
+
+def _recv_hello(sock, world_size: int, token: bytes) -> int:
+    """Raw-bytes hello (no unpickling): magic, rank, the job token."""
+    head = _recv_exact(sock, 10)
+    if head[:4] != _HELLO_MAGIC:
+        raise ConnectionError("control-plane hello has the wrong magic")
+    rank, ntok = struct.unpack("!IH", head[4:])
+    if ntok > _MAX_TOKEN:
+        raise ConnectionError("control-plane hello token too long")
+    got = _recv_exact(sock, ntok)
+    if not hmac.compare_digest(got, token):
+        raise ConnectionError("control-plane hello with a foreign job token")
+    if not 0 < rank < world_size:
+        raise ConnectionError(f"control-plane hello from rank {rank} of {world_size}")
+    return rank
 
 
 class Group:
     """Star-shaped host control plane over TCP (no torch, no MPI).
 
     Every rank calls the same collectives in the same order. Rank 0 accepts
-    WORLD_SIZE - 1 connections; messages are length-prefixed pickles exchanged
-    between the ranks of one job only."""
+    WORLD_SIZE - 1 connections. A connection is admitted only after a raw-bytes
+    hello carrying the job token (job_token()); only then are messages --
+    length-prefixed pickles, at most MAX_MESSAGE bytes -- exchanged."""
 
     def __init__(self, rank: int, world_size: int, addr: str = "127.0.0.1", port: int | None = None,
                  timeout: float = 300.0):
@@ -112,14 +151,22 @@ class Group:
             srv.listen(world_size)
             srv.settimeout(timeout)
             peers: list[socket.socket | None] = [None] * world_size
+            token = job_token()
+            deadline = time.monotonic() + timeout
             try:
-                for _ in range(world_size - 1):
+                while any(p is None for p in peers[1:]):
+                    srv.settimeout(max(0.01, deadline - time.monotonic()))
                     conn, _ = srv.accept()
-                    conn.settimeout(timeout)
+                    conn.settimeout(min(timeout, 30.0))
                     conn.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-                    r = _recv(conn)
-                    if not (isinstance(r, int) and 0 < r < world_size) or peers[r] is not None:
-                        raise ConnectionError(f"unexpected control-plane hello {r!r}")
+                    try:
+                        r = _recv_hello(conn, world_size, token)
+                        if peers[r] is not None:
+                            raise ConnectionError(f"second control-plane hello from rank {r}")
+                    except (ConnectionError, OSError):
+                        conn.close()  # not one of this job's ranks: drop it, keep listening
+                        continue
+                    conn.settimeout(timeout)
                     peers[r] = conn
             finally:
                 srv.close()
@@ -136,7 +183,7 @@ class Group:
                     time.sleep(0.05)
             s.settimeout(timeout)
             s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-            _send(s, rank)
+            _send_hello(s, rank, job_token())
             self.sock = s
 
     @classmethod

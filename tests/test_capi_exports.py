@@ -52,3 +52,26 @@ def test_version_and_lengths_without_device():
         assert lib.slm_supported_length(n) == 1
     for n in (0, 100, 300, 8192):
         assert lib.slm_supported_length(n) == 0
+
+
+def test_gather_layout_offsets_match_the_shards():
+    """slm_gather_layout is the offset arithmetic of slm_plan_gather_phase /
+    slm_plan_gather_stats (rank order, per-hologram slabs); host-only, so it
+    runs here. It must place rank r's slab where parallel.shard_range puts
+    rank r's holograms."""
+    from spatial_light_modulator_module_amd import parallel
+
+    import numpy as np
+    import pytest
+
+    for total, nranks in [(512, 8), (64, 8), (7, 3), (1, 2), (0, 2), (3, 5)]:
+        counts = parallel.shard_counts(total, nranks)
+        for per_item in (1, 4 * 200, 1024 * 1024):
+            off = _lib.gather_layout(counts, per_item)
+            assert off.shape == (nranks + 1,) and off[-1] == total * per_item
+            for r in range(nranks):
+                rng = parallel.shard_range(total, nranks, r)
+                assert off[r] == rng.start * per_item and off[r + 1] - off[r] == len(rng) * per_item
+    np.testing.assert_array_equal(_lib.gather_layout([3, 0, 2], 7), [0, 21, 21, 35])
+    with pytest.raises(_lib.SlmError):
+        _lib.gather_layout([2, -1], 4)

@@ -185,3 +185,55 @@ def test_sequence_cli_two_ranks_matches_single(tmp_path, monkeypatch):
     for r in (0, 1):
         np.testing.assert_array_equal(np.load(two / f"errors_rank{r}.npy"),
                                       np.array([errors[i] for i in range(n)]))
+
+
+def test_control_plane_admits_only_this_jobs_ranks(monkeypatch):
+    """Rank 0 reads a raw-bytes hello (magic, rank, job token) before it
+    unpickles anything: a foreign client -- a pickle payload, a wrong token, an
+    oversized length prefix -- is dropped and the real rank 1 still joins."""
+    import pickle
+    import socket
+    import struct
+    import threading
+
+    monkeypatch.setenv("SLM_JOB_TOKEN", "job-a")
+    port = _free_port()
+    box = {}
+
+    def rank0():
+        box["g0"] = parallel.Group(0, 2, "127.0.0.1", port, timeout=30)
+
+    th = threading.Thread(target=rank0)
+    th.start()
+    import time
+
+    deadline = time.monotonic() + 10
+    while True:  # rank 0 listening?
+        try:
+            probe = socket.create_connection(("127.0.0.1", port), timeout=1)
+            break
+        except OSError:
+            assert time.monotonic() < deadline
+            time.sleep(0.02)
+    evil = pickle.dumps(1)  # a pickle instead of a hello
+    probe.sendall(struct.pack("!Q", len(evil)) + evil)
+    probe.close()
+    wrong = socket.create_connection(("127.0.0.1", port), timeout=5)
+    parallel._send_hello(wrong, 1, b"job-b")  # right shape, foreign token
+    wrong.close()
+    huge = socket.create_connection(("127.0.0.1", port), timeout=5)
+    huge.sendall(b"SLMh" + struct.pack("!IH", 1, 65535))  # token length beyond the cap
+    huge.close()
+    g1 = parallel.Group(1, 2, "127.0.0.1", port, timeout=30)
+    th.join(30)
+    g0 = box["g0"]
+    out = {}
+    t2 = threading.Thread(target=lambda: out.setdefault(0, g0.all_gather("zero")))
+    t2.start()
+    assert g1.all_gather("one") == ["zero", "one"]
+    t2.join(10)
+    assert out[0] == ["zero", "one"]
+    with pytest.raises(ValueError):
+        parallel._send(g1.sock, b"x" * (parallel.MAX_MESSAGE + 1))
+    g0.close()
+    g1.close()

@@ -74,21 +74,30 @@ def test_gd_gif_frames_vs_oracle(gpu, tmp_path, gif_type):
 
 
 @pytest.mark.gpu
-def test_gs_gif_frames(gpu, tmp_path):
+@pytest.mark.parametrize("gif_type", ["h", "i"])
+def test_gs_gif_frames(gpu, tmp_path, gif_type):
+    """add_gif_image (src/algorithms.py:52-57): "h" frames are the phase of A,
+    "i" frames the normalised expected_outcome |C|^2 norm / max (:36-37), both
+    PIL 'L' images of the iteration's state."""
     from spatial_light_modulator_module_amd.algorithms import gerchberg_saxton
 
     rng = np.random.default_rng(8)
     t = rng.integers(0, 256, (128, 128)).astype(np.uint8)
-    a = _args(tmp_path, gif_type="h", max_loops=9, gif_skip=4)
+    a = _args(tmp_path, gif_type=gif_type, max_loops=9, gif_skip=4)
     holo, exp, err = gerchberg_saxton(t, a)
     assert len(err) == 9
     assert sorted(os.listdir(tmp_path)) == ["0.png", "1.png", "2.png"]  # iterations 0, 4, 8
-    ph1, _, err1 = orc.gerchberg_saxton_faithful(t, 1)
-    want = np.array(Image.fromarray((ph1 + np.pi) * 256 / (2 * np.pi)).convert("L"), dtype=np.int16)
+    ph1, exp1, err1 = orc.gerchberg_saxton_faithful(t, 1)
+    if gif_type == "h":
+        want = np.array(Image.fromarray((ph1 + np.pi) * 256 / (2 * np.pi)).convert("L"), dtype=np.int16)
+        last = np.array(Image.fromarray((holo + np.pi) * 256 / (2 * np.pi)).convert("L"), dtype=np.int16)
+    else:
+        assert exp1.dtype == np.float64 and np.isclose(exp1.max(), t.max())
+        want = np.array(Image.fromarray(exp1).convert("L"), dtype=np.int16)
+        last = np.array(Image.fromarray(exp).convert("L"), dtype=np.int16)
     _close_frames(_frame(tmp_path / "0.png"), want)
     np.testing.assert_allclose(err[0], err1[0], rtol=1e-5)
-    # the last frame is the returned hologram's image
-    last = np.array(Image.fromarray((holo + np.pi) * 256 / (2 * np.pi)).convert("L"), dtype=np.int16)
+    # the last frame is the image of the returned hologram / expected outcome
     np.testing.assert_array_equal(_frame(tmp_path / "2.png"), last)
 
 
