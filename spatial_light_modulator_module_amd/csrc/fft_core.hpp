@@ -272,9 +272,15 @@ __device__ __forceinline__ int lds_slot(int o) {
 #endif
 }
 
-template <class X, int ALT = 0>
+// WAVE: every line of the region is written and read by the threads of one
+// wave only (wave-line mappings, kernels.hpp), so an exchange needs no
+// workgroup barrier: the wave waits for its own LDS writes (lgkmcnt) and
+// reads; the next pass's writes cannot pass this pass's reads (a wave's LDS
+// operations execute in order).
+template <class X, int ALT = 0, bool WAVE = false>
 struct LdsLine {  // per-line LDS regions `stride` apart (row kernels; columns of one-group tiles)
-    static constexpr bool kDouble = ALT > 0;
+    static constexpr bool kDouble = ALT > 0 && !WAVE;
+    static constexpr bool kWave = WAVE;
     X* base;
     int stride = 0;
     mutable int cur = 0;
@@ -290,9 +296,10 @@ struct LdsLine {  // per-line LDS regions `stride` apart (row kernels; columns o
     }
 };
 
-template <int CW, class X, int ALT = 0>
+template <int CW, class X, int ALT = 0, bool WAVE = false>
 struct LdsTile {  // CW interleaved columns (column kernels): [o][c]; the thread's lines are c + l
-    static constexpr bool kDouble = ALT > 0;
+    static constexpr bool kDouble = ALT > 0 && !WAVE;
+    static constexpr bool kWave = WAVE;  // as LdsLine: every line's threads in one wave
     static constexpr int kCW = CW, kAlt = ALT;
     X* base;
     int c;
@@ -504,13 +511,32 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
 }
-__device__ __forceinline__ void exchange_barrier() { lds_barrier(); }
+// Wave-local exchange point: this wave's LDS writes have landed; no s_barrier.
+__device__ __forceinline__ void wave_lds_sync() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+}
+// between the writes and the reads of one exchange
+template <class Lds>
+__device__ __forceinline__ void exchange_sync(const Lds&) {
+    if constexpr (Lds::kWave)
+        wave_lds_sync();
+    else
+        lds_barrier();
+}
+// after the reads of one exchange, before the next exchange's writes
 template <class Lds>
 __device__ __forceinline__ void exchange_done(const Lds& lds) {
-    if constexpr (Lds::kDouble)
+    if constexpr (Lds::kWave) {
+        asm volatile("" ::: "memory");  // keep the next writes behind these reads in program order
+    } else if constexpr (Lds::kDouble) {
         lds.flip();
-    else
-        exchange_barrier();
+    } else {
+        lds_barrier();
+    }
 }
 
 // ------------------------------------------------------------------------
@@ -578,7 +604,7 @@ __device__ __forceinline__ void stockham_from(V (&v)[L][E], int t, const Tw& tw,
 #endif
     });
     if constexpr (sizeof...(Rest) > 0) {
-        exchange_barrier();
+        exchange_sync(lds);
         static_for<L>([&](auto lc) {
             constexpr int l = decltype(lc)::value;
             static_for<E>([&](auto mc) {
@@ -703,7 +729,7 @@ __device__ __forceinline__ void fft_pair(V (&v)[L][PlanOf<K>::E], int t, const T
             });
         };
         stockham_all<K, INV1, C>(v, t, tw, lds, sink, RadicesOf<K>{});
-        exchange_barrier();
+        exchange_sync(lds);
         static_for<L>([&](auto lc) {
             constexpr int l = decltype(lc)::value;
             static_for<E>([&](auto mc) {

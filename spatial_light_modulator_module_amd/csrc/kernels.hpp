@@ -149,6 +149,32 @@ constexpr int kLdsPair = 80 * 1024;
 #ifndef SLM_ROW_LINES2_MIN_N
 #define SLM_ROW_LINES2_MIN_N 8192  // off: 8 x 4096^2 row pass 695 -> 843 us with row pairs in-thread
 #endif
+// Wave-local exchanges: where every thread of a line sits in one wave, a
+// Stockham exchange needs no workgroup barrier -- LDS writes, s_waitcnt, LDS
+// reads (fft_core.hpp, exchange_sync). That holds with the default lane maps
+// for rows of T <= 16 threads and for column tiles of T x CW / L <= 64 threads
+// (SLM_WAVE_LOCAL); rows of T = 32 are remapped so each row is one half-wave
+// (SLM_WAVE_LINE, T consecutive lanes per row). Measured per launch (f32,
+// tools/kt.py, gpurun_out/s6): rows 256^2 x 64 15.66 -> 14.33 us, one 256^2
+// 4.24 -> 3.98 us, 16 x 512^2 23.45 -> 22.95 us; remapping rows of T = 64
+// (1024 wide) was slower (64 x 1024^2 260 -> 276 us), and so was remapping
+// columns to one column per wave (64 x 1024^2 265 -> 567 us: a wave then reads
+// 8 B per lane at a 32-B stride), so neither is done.
+#ifndef SLM_WAVE_LOCAL
+#define SLM_WAVE_LOCAL 1
+#endif
+#ifndef SLM_WAVE_LINE
+#define SLM_WAVE_LINE 1
+#endif
+template <int K>
+constexpr bool row_wave_remap(int lines_per_thread) {
+    return SLM_WAVE_LOCAL && SLM_WAVE_LINE && lines_per_thread == 1 && PlanOf<K>::T == 32;
+}
+template <int K>
+constexpr bool row_wave_local(int lines_per_thread) {
+    return SLM_WAVE_LOCAL && lines_per_thread == 1 && (PlanOf<K>::T <= 16 || row_wave_remap<K>(lines_per_thread));
+}
+
 template <int K, bool COL>
 constexpr int lines_of() {
     return (kPlans[K].variant == 1 && PlanOf<K>::N >= (COL ? SLM_COL_LINES2_MIN_N : SLM_ROW_LINES2_MIN_N)) ? 2 : 1;
@@ -176,6 +202,8 @@ struct RowCfg {
     static constexpr int RPW = (T >= 64) ? (kSingle ? 1 : kPairs ? 2 : 4) : 256 / T;
 #endif
     static_assert(RPW % L == 0, "rows per workgroup must be a multiple of the rows per thread");
+    static constexpr bool kWave = row_wave_local<K>(L);    // each row inside one wave (wave-local exchanges)
+    static constexpr bool kRemap = row_wave_remap<K>(L);   // ... by T consecutive lanes per row
     static constexpr int RL = RPW / L;              // row groups across lanes
     static constexpr int QR = RL < 4 ? RL : 4;      // rows interleaved across a wave
     static constexpr int THREADS = RL * T;
@@ -186,6 +214,7 @@ struct ColCfg {
     static constexpr int T = PlanOf<K>::T;
     static constexpr int L = (CW % 2 == 0) ? lines_of<K, true>() : 1;  // columns per thread
     static constexpr int THREADS = (CW / L) * T;
+    static constexpr bool kWave = SLM_WAVE_LOCAL && T * (CW / L) <= 64;  // each column inside one wave
     static constexpr bool kValid =
         THREADS >= 64 && THREADS <= 1024 && lds_line(PlanOf<K>::N) * CW * 8 <= 160 * 1024;
 };
@@ -631,6 +660,11 @@ constexpr bool kLdsDouble = SLM_LDS_DOUBLE && K == 11;
 template <int K, int P>
 constexpr int row_wpe() {
     using X = XchgOf<P, (long long)RowCfg<K>::RPW * PlanOf<K>::ROWSTRIDE, K>;
+    // per-plan waves-per-SIMD floor for the float32 row kernels (register budget
+    // 512 / w; A/B knob: -DSLM_ROW_WPE_K=<key> -DSLM_ROW_WPE=<w>)
+#if defined(SLM_ROW_WPE_K) && defined(SLM_ROW_WPE)
+    if constexpr (K == SLM_ROW_WPE_K && P == 0) return SLM_ROW_WPE;
+#endif
     return occupancy_wpe(RowCfg<K>::THREADS,
                          (kLdsDouble<K, false> ? 2 : 1) * (long long)RowCfg<K>::RPW * PlanOf<K>::ROWSTRIDE * sizeof(X));
 }
@@ -658,14 +692,21 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
     // blocked layout, and a 16-lane LDS write group stays inside one row. A
     // thread carries rows lrow * L + l, l < L.
     constexpr int QR = RowCfg<K>::QR;
-    const int tlo = threadIdx.x % TL;
-    const int q4 = (threadIdx.x / TL) % QR;
-    const int rest = threadIdx.x / (QR * TL);
-    const int qq = rest / (T / TL);
-    const int t = tlo + TL * (rest - qq * (T / TL));
-    const int lrow = (qq * QR + q4) * L;
+    constexpr bool WV = RowCfg<K>::kWave;
+    int t, lrow;
+    if constexpr (RowCfg<K>::kRemap) {  // wave-line: T consecutive lanes per row, rows never cross a wave
+        t = threadIdx.x % T;
+        lrow = threadIdx.x / T;
+    } else {
+        const int tlo = threadIdx.x % TL;
+        const int q4 = (threadIdx.x / TL) % QR;
+        const int rest = threadIdx.x / (QR * TL);
+        const int qq = rest / (T / TL);
+        t = tlo + TL * (rest - qq * (T / TL));
+        lrow = (qq * QR + q4) * L;
+    }
     const long long bstep = (long long)T * p.H;  // slot m adds m * bstep (blocked layout)
-    const LdsLine<X, ALT> lds{smem + lrow * LINE, LINE};
+    const LdsLine<X, WV ? 0 : ALT, WV> lds{smem + lrow * LINE, LINE};
     if constexpr (MODE == ROW_GS_MAIN || MODE == ROW_GD_MAIN || MODE == ROW_GD_LIN) trace_entry(p.trace);
     sgpr_pin(p.in, p.out, p.holo, p.H, p.B, p.ntile, p.tw, p.ain, p.wt, gridDim.x);
     Twiddles<K, C, tw_mode<P, RowCfg<K>::THREADS, K, false>()> tw;
@@ -876,7 +917,9 @@ __device__ __forceinline__ void gd_inverse_pair(V (&wu)[L][E], V (&wv)[L][E], in
                 w2[l][m] = wu[l][m];
                 w2[L + l][m] = wv[l][m];
             }
-        // the same buffer alternation continues (kDouble exchanges)
+        // the same buffer alternation continues (kDouble exchanges); a wave-local
+        // region hands over to the wider, workgroup-synchronised one at a barrier
+        if constexpr (Lds::kWave) lds_barrier();
         const LdsTile<2 * Lds::kCW, X, Lds::kAlt> lds2{smem, 2 * c, lds.cur};
         fft_line<K, true, C>(w2, t, tw, lds2);
 #pragma unroll
@@ -918,6 +961,9 @@ constexpr int col_lds_width() {
 template <int K, int CW, int P, int MODE = COL_GS_MAIN>
 constexpr int col_wpe() {
     using X = XchgOf<P, (long long)PlanOf<K>::LINE * CW, K>;
+#if defined(SLM_COL_WPE_K) && defined(SLM_COL_WPE)
+    if constexpr (K == SLM_COL_WPE_K && P == 0) return SLM_COL_WPE;
+#endif
     return occupancy_wpe(ColCfg<K, CW>::THREADS, (kLdsDouble<K, true> ? 2 : 1) * (long long)PlanOf<K>::LINE *
                                                      col_lds_width<K, CW, P, MODE>() * sizeof(X));
 }
@@ -937,7 +983,10 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P, M
     using V = StateOf<P, X>;
     constexpr int LW = col_lds_width<K, CW, P, MODE>();  // exchange columns (2 CW: COL_GD_LIN's paired inverses)
     constexpr int ALT = kLdsDouble<K, true> ? LINE * LW : 0;
-    __shared__ X smem[(ALT ? 2 : 1) * LINE * LW];
+    constexpr bool WV = ColCfg<K, CW>::kWave;
+    constexpr int RS = PlanOf<K>::ROWSTRIDE;  // line-major regions (one-group tiles)
+    constexpr int SMEM = (ALT ? 2 : 1) * LINE * LW > CW * RS ? (ALT ? 2 : 1) * LINE * LW : CW * RS;
+    __shared__ X smem[SMEM];
 
     // a thread carries columns c .. c + L - 1 of the tile (adjacent in the
     // blocked layout: one 16-B access for L = 2)
@@ -946,11 +995,11 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P, M
     // inputs (X, target) in layout X, outputs (Y) in layout Y: row y = t + T m
     constexpr long long kStep = (long long)kPanelOf<LAYOUT_X> * T;
     constexpr long long kStepY = (long long)kPanelOf<LAYOUT_Y> * T;
-    using LdsT = std::conditional_t<kColLineMajor<K, CW>, LdsLine<X, ALT>, LdsTile<CW, X, ALT>>;
-    static_assert(!kColLineMajor<K, CW> || PlanOf<K>::ROWSTRIDE * CW <= LINE * LW, "line-major region fits");
+    using LdsT = std::conditional_t<kColLineMajor<K, CW>, LdsLine<X, WV ? 0 : ALT, WV>,
+                                    LdsTile<CW, X, WV ? 0 : ALT, WV>>;
     const LdsT lds = [&] {
         if constexpr (kColLineMajor<K, CW>)
-            return LdsT{smem, PlanOf<K>::ROWSTRIDE};  // c == 0: the thread's lines are its columns
+            return LdsT{smem, RS};  // c == 0: the thread's lines are its columns
         else
             return LdsT{smem, c};
     }();

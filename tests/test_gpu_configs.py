@@ -138,12 +138,18 @@ def test_gs_4096_warm_start_gate(gpu):
 
     At 4096^2 the warm-started iteration is still chaotic: a float32 build's
     one-step error (1.6e-7 rms) grows ~x1.045 per iteration, so after 100
-    iterations the distance to float64 is a wide random variable (measured
-    9.7e-6 .. 2.8e-5 across builds whose one-step errors agree to 0.1 %,
-    tools/diag_step.py). Gates: float32 butterflies (the default) at +50
-    (<= 1e-5; SURVEY 8c measured 1.4e-6 for a complex64 model), float64
-    butterflies at +100 (<= 1e-5); the float32 +100 value is reported and held
-    to the chaotic band (<= 5e-5). Error curves within 5e-4 relative."""
+    iterations the distance to float64 depends on the exact rounding sequence
+    of the build (9.7e-6 .. 2.8e-5 measured across arithmetic variants whose
+    one-step errors agree to 0.1 %, tools/diag_step.py). A float32 FFT cannot
+    shrink that one-step error enough to make every variant pass: its rms
+    error is set by the float32 additions (tools/fft_precision_sim.py: exact
+    twiddles 1.27e-7 -> 1.20e-7, float64 butterflies 4.4e-8), and float64
+    butterflies cost 1.75x at 4096^2. The shipped
+    build's arithmetic is deterministic (exchange layouts move addresses,
+    never values), so its +100 value is a fixed number (6.94e-6 in r02 and
+    r03), held here to the north-star bar: any change of the 4096 kernels'
+    arithmetic must pass this gate again. Gates: float32 +50 and +100, float64
+    +50 and +100, all <= 1e-5; error curves within 5e-4 relative."""
     lib = gpu
     n = 4096
     t = bench_targets(0, 1, n)
@@ -169,7 +175,7 @@ def test_gs_4096_warm_start_gate(gpu):
         f"{p} +{s}: phase rms {rms[(p, s)]:.3e} err rel {errs[(p, s)]:.1e}" for p in ("f32", "f64") for s in (50, 100)))
     assert rms[("f32", 50)] < PHASE_RMS_TOL
     assert rms[("f64", 100)] < PHASE_RMS_TOL
-    assert rms[("f32", 100)] < 5e-5
+    assert rms[("f32", 100)] < PHASE_RMS_TOL
     assert max(errs.values()) < 5e-4
 
 
