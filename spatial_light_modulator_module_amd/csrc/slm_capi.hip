@@ -365,6 +365,10 @@ int pick_plan(int n, long long elems, int prec, bool row = false) {
     // every batch (gpurun_out/exp19: 1 image 26.7 -> 21.7 us, 16 images
     // 405 -> 292 us per row launch); columns keep the rule below
     if (row && prec == PREC_F32 && n == 2048) return narrow;
+    // float64 4096-point rows: the 3-pass E = 16 plan (one row per workgroup)
+    // beats the 4-pass E = 32 one (gpurun_out/s5: 4096^2 row pass 180 -> 142 us,
+    // columns keep the wide plan: 200 vs 238 us)
+    if (row && prec == PREC_F64 && n == 4096) return narrow;
     const long long waves = elems / kPlans[wide].e / 64;
     return waves < 4LL * 1024 ? narrow : wide;
 }

@@ -85,3 +85,45 @@ def test_gather_stats_single_rank(gpu):
         with lib.Plan(lib.ALGO_GS, 3, 256, 256, lib.TGT_F32, False, loops) as p:
             p.set_target(t)
             p.gather_stats([2], 0)
+
+
+def _integration_batch_binding(path):
+    """INTEGRATION.md's slm_gs_multi stub, as a maintainer would paste it."""
+    import ctypes
+
+    _lib = ctypes.CDLL(path)
+    _vp, _i, _d = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
+    _lib.slm_last_error.restype = ctypes.c_char_p
+    _lib.slm_gs_multi.argtypes = [_i, _vp, _vp, _i, _vp, _i, _i, _i, _i, _d, _vp, _vp, _vp, _vp, _vp]
+    SLM_TGT_U8, SLM_TGT_F32 = 0, 1
+
+    def _p(a):
+        return None if a is None else a.ctypes.data
+
+    def gerchberg_saxton_batch_hip(targets, max_loops, devices=(0, 1, 2, 3, 4, 5, 6, 7)):
+        t = np.ascontiguousarray(targets)
+        tt = SLM_TGT_U8 if t.dtype == np.uint8 else SLM_TGT_F32
+        if tt == SLM_TGT_F32:
+            t = t.astype(np.float32)
+        b, h, w = t.shape
+        dev = np.ascontiguousarray(devices, np.int32)
+        phase = np.empty((b, h, w), np.float32)
+        stats = np.empty((b, max_loops, 4), np.float64)
+        rc = _lib.slm_gs_multi(len(dev), _p(dev), _p(t), tt, None, b, h, w, max_loops, 0.0, None,
+                               _p(phase), None, _p(stats), None)
+        if rc != 0:
+            raise RuntimeError(_lib.slm_last_error().decode())
+        return phase.astype(np.float64), [list(s[:, 3]) for s in stats]
+
+    return gerchberg_saxton_batch_hip
+
+
+@pytest.mark.gpu
+def test_gs_multi_as_integration_binds_it(gpu):
+    lib = gpu
+    batch_hip = _integration_batch_binding(lib.LIB_PATH)
+    t = _targets(6, 128, True)
+    ph, errs = batch_hip(t, 10, devices=(0, 0, 0, 0))
+    rph, _, rst, _ = _whole_batch(lib, t, 10)
+    np.testing.assert_array_equal(ph, rph.astype(np.float64))
+    assert errs == [list(s[:, 3]) for s in rst]
