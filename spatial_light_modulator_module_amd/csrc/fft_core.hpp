@@ -351,7 +351,12 @@ struct TwCountOf<N, IntList<Rs...>> {
 //             far below the complex64 storage rounding).
 //  TW_CHAIN:  as TW_POWERS, but w^r is formed incrementally as it is applied
 //             (w^r = w^(r-1) w), so only two twiddles are ever live.
-enum TwMode : int { TW_CACHED = 0, TW_DIRECT = 1, TW_POWERS = 2, TW_CHAIN = 3 };
+//  TW_LAST:   the last pass's twiddles (one per butterfly output: the most
+//             distinct values per thread) cached in registers, earlier passes
+//             read from the (L1-resident, few-KB) table where used -- the same
+//             values as TW_CACHED, so the same results bit for bit, with
+//             (R - 1) x (earlier passes) fewer registers.
+enum TwMode : int { TW_CACHED = 0, TW_DIRECT = 1, TW_POWERS = 2, TW_CHAIN = 3, TW_LAST = 4 };
 
 template <int N, int Ns, int... Rs>
 struct TwPowCountImpl;
@@ -459,6 +464,54 @@ struct Twiddles<N, C, TW_CHAIN> {
     }
 };
 
+// TW_LAST: register slots of the last pass only
+template <int N, int Ns, int... Rs>
+struct TwLastCountImpl;
+template <int N, int Ns, int R>
+struct TwLastCountImpl<N, Ns, R> {
+    static constexpr int value = Ns > 1 ? (PlanOf<N>::E / R) * (R - 1) : 0;
+};
+template <int N, int Ns, int R, int R2, int... Rest>
+struct TwLastCountImpl<N, Ns, R, R2, Rest...> {
+    static constexpr int value = TwLastCountImpl<N, Ns * R, R2, Rest...>::value;
+};
+template <int N, class L>
+struct TwLastCountOf;
+template <int N, int... Rs>
+struct TwLastCountOf<N, IntList<Rs...>> {
+    static constexpr int value = TwLastCountImpl<N, 1, Rs...>::value;
+};
+
+template <int N, class C>
+struct Twiddles<N, C, TW_LAST> {
+    static constexpr int COUNT = TwLastCountOf<N, RadicesOf<N>>::value > 0 ? TwLastCountOf<N, RadicesOf<N>>::value : 1;
+    struct alignas(2 * sizeof(Scalar<C>)) Pod {
+        Scalar<C> x, y;
+    };
+    using GlobalPtr = const __attribute__((address_space(1))) Pod*;
+    C w[COUNT];
+    GlobalPtr table;
+    __device__ __forceinline__ void launder() {
+        unsigned long long q = (unsigned long long)table;
+        asm volatile("" : "+s"(q));
+        table = (GlobalPtr)q;
+    }
+    template <int TwOff, int RegOff, int PowOff, int R, int Ns, bool INV>
+    __device__ __forceinline__ void apply(C* u, int k, int j) const {
+        static_for<R - 1>([&](auto rc) {
+            constexpr int r = decltype(rc)::value + 1;
+            C t;
+            if constexpr (Ns * R == PlanOf<N>::N) {
+                t = w[k * (R - 1) + r - 1];
+            } else {
+                const int i = TwOff + (r - 1) * Ns + j;
+                t = mk<C>(table[i].x, table[i].y);
+            }
+            u[r] = INV ? cmulc(u[r], t) : cmul(u[r], t);
+        });
+    }
+};
+
 template <int N, class C, int MODE, int E, int Ns, int TwOff, int RegOff, int PowOff, int R, int... Rest>
 __device__ __forceinline__ void load_twiddles_pass(Twiddles<N, C, MODE>& tw, int t, const C* __restrict__ table) {
     constexpr int T = PlanOf<N>::T;  // N is the plan key here
@@ -472,6 +525,13 @@ __device__ __forceinline__ void load_twiddles_pass(Twiddles<N, C, MODE>& tw, int
                     constexpr int r = decltype(rc)::value;
                     tw.w[RegOff + k * (R - 1) + r] = table[TwOff + r * Ns + j];
                 });
+            } else if constexpr (MODE == TW_LAST) {
+                if constexpr (sizeof...(Rest) == 0) {
+                    static_for<R - 1>([&](auto rc) {
+                        constexpr int r = decltype(rc)::value;
+                        tw.w[k * (R - 1) + r] = table[TwOff + r * Ns + j];
+                    });
+                }
             } else {
                 tw.w1[PowOff + k] = table[TwOff + j];  // r = 1 entry
             }
@@ -490,9 +550,9 @@ __device__ __forceinline__ void load_twiddles_impl(Twiddles<N, C, MODE>& tw, int
 }
 template <int N, class C, int MODE>
 __device__ __forceinline__ void load_twiddles(Twiddles<N, C, MODE>& tw, int t, const void* table) {
-    if constexpr (MODE == TW_DIRECT)
+    if constexpr (MODE == TW_DIRECT || MODE == TW_LAST)
         tw.table = (typename Twiddles<N, C, MODE>::GlobalPtr)table;
-    else
+    if constexpr (MODE != TW_DIRECT)
         load_twiddles_impl<N, C, MODE>(tw, t, static_cast<const C*>(table), RadicesOf<N>{});
 }
 
