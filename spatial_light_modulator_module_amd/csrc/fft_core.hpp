@@ -351,11 +351,13 @@ struct TwCountOf<N, IntList<Rs...>> {
 //             far below the complex64 storage rounding).
 //  TW_CHAIN:  as TW_POWERS, but w^r is formed incrementally as it is applied
 //             (w^r = w^(r-1) w), so only two twiddles are ever live.
-//  TW_LAST:   the last pass's twiddles (one per butterfly output: the most
-//             distinct values per thread) cached in registers, earlier passes
-//             read from the (L1-resident, few-KB) table where used -- the same
-//             values as TW_CACHED, so the same results bit for bit, with
-//             (R - 1) x (earlier passes) fewer registers.
+//  TW_LAST:   the last pass's twiddles cached in registers, earlier passes
+//             read from the (L1-resident, few-KB) table where used: fewer
+//             registers (4096 row kernel 194 -> 165 VGPRs, 3 waves per SIMD)
+//             but measured slower (4096^2 row pass 103 -> 117 us, 8 x 4096^2
+//             785 -> 968 us: the table loads sit in the dependency chain), and
+//             the compiler contracts the products differently (not bitwise
+//             TW_CACHED). Kept for A/B builds (-DSLM_F32_ROW_TW=4).
 enum TwMode : int { TW_CACHED = 0, TW_DIRECT = 1, TW_POWERS = 2, TW_CHAIN = 3, TW_LAST = 4 };
 
 template <int N, int Ns, int... Rs>
