@@ -180,6 +180,21 @@ def run_gs(targets, loops, tol=0.0, ain=None, initial_phase=None):
     return _collect(plan, phase, e, stats, iters, loops, checked)
 
 
+def run_gs_multi(targets, loops, devices, tol=0.0, ain=None):
+    """run_gs's contract over several GPUs from this one process
+    (slm_gs_multi: contiguous shards, one host thread / plan per device)."""
+    t = np.asarray(targets)
+    tdev, _ = target_for_device(t)
+    phase, e, stats, iters = _lib.gs_multi(tdev, loops, devices, tol=tol, ain=ain)
+    norm = t.reshape(t.shape[0], -1).max(axis=1).astype(np.float64)  # np.amax(demanded_output)
+    errs, maxes = [], []
+    for k in range(t.shape[0]):
+        n = loops if iters[k] < 0 else int(iters[k])
+        errs.append([np.float64(v) for v in stats[k, :n, 3]])
+        maxes.append(stats[k, n - 1, 0])
+    return phase, e, errs, norm, np.array(maxes)
+
+
 def _collect(plan, phase, e, stats, iters, loops, checked):
     norm, _ = plan.target_stats()
     errs, maxes = [], []

@@ -9,8 +9,10 @@ one-process-per-GPU launcher (torch.distributed.run or any that sets RANK /
 WORLD_SIZE / MASTER_ADDR / MASTER_PORT) each rank takes a contiguous shard of
 the frames (parallel.shard_range) and writes its own .npy files: no collective
 touches the data path; only the per-frame error lists travel, over the
-torch-free control plane (parallel.Group). Output files, names and stdout lines
-are the reference's.
+torch-free control plane (parallel.Group). Without a launcher, $SLM_GPUS (a
+device count, "all", or a comma-separated device list) runs each batch over
+several GPUs from this one process instead (slm_gs_multi).
+Output files, names and stdout lines are the reference's.
 """
 from __future__ import annotations
 
@@ -21,7 +23,9 @@ import sys
 import numpy as np
 
 from . import parallel
-from .algorithms import _check_shape, _print_loops, expected_from, hologram_from, incoming_amplitude, run_gs
+from . import _lib
+from .algorithms import (_check_shape, _print_loops, expected_from, hologram_from, incoming_amplitude, run_gs,
+                         run_gs_multi)
 
 SEQ_BATCH = int(os.environ.get("SLM_SEQ_BATCH", "64"))  # frames per GPU launch batch
 
@@ -45,6 +49,18 @@ def _batches(indices, frames):
         yield run
 
 
+def multi_devices(nranks):
+    """Devices for one-process multi-GPU batches ($SLM_GPUS), or None."""
+    spec = os.environ.get("SLM_GPUS", "").strip()
+    if not spec or nranks > 1:
+        return None
+    if "," in spec:
+        devs = [int(d) for d in spec.split(",") if d.strip()]
+    else:
+        devs = list(range(_lib.device_count() if spec == "all" else int(spec)))
+    return devs if len(devs) > 1 else None
+
+
 def generate_hologram_sequence(args, rank=None, nranks=None):
     """src/generate_hologram_sequence.py:10-31. Returns the per-frame error
     evolutions of the frames this rank computed (dict frame -> list)."""
@@ -61,13 +77,17 @@ def generate_hologram_sequence(args, rank=None, nranks=None):
     mine = list(parallel.shard_range(n_files, nranks, rank))
     frames = {i: _load_frame(source_dir_path, i) for i in mine}
     errors = {}
+    devices = multi_devices(nranks)
     for idx in _batches(mine, frames):
         stack = np.stack([frames[i] for i in idx])
         _check_shape(stack[0])
         ain = incoming_amplitude(args, stack.shape[1:])
         if not (args.max_loops > 0 and (args.tolerance + 1) > args.tolerance):
             raise UnboundLocalError("local variable 'expected_outcome' referenced before assignment")
-        phase, e, errs, norm, emax = run_gs(stack, args.max_loops, args.tolerance, ain)
+        if devices:
+            phase, e, errs, norm, emax = run_gs_multi(stack, args.max_loops, devices, args.tolerance, ain)
+        else:
+            phase, e, errs, norm, emax = run_gs(stack, args.max_loops, args.tolerance, ain)
         for k, i in enumerate(idx):
             sys.stdout.write(f"\rcreating {i}. hologram ")
             _print_loops(len(errs[k]), args.max_loops)

@@ -114,3 +114,38 @@ def test_generate_hologram_sequence_cli(gpu, tmp_path, monkeypatch):
         prev = np.array(Image.open(tmp_path / "images" / "moving_traps" / "walk_a_preview" / f"{i}.png"))
         want = np.array(Image.fromarray(exp).convert("L"))
         assert prev.shape == want.shape and np.mean(prev != want) < 1e-3
+
+
+@pytest.mark.gpu
+def test_generate_hologram_sequence_cli_one_process_multi_gpu(gpu, tmp_path, monkeypatch):
+    """$SLM_GPUS without a launcher: each frame batch runs through slm_gs_multi
+    (shards on the listed devices -- one GPU listed twice here); the written
+    holograms, previews and error lists equal the single-device CLI's."""
+    from spatial_light_modulator_module_amd import generate_hologram_sequence as ghs
+
+    monkeypatch.chdir(tmp_path)
+    rng = np.random.default_rng(19)
+    frames = [_trap_image(rng, 256, 512) for _ in range(5)]
+    for root in ("one", "multi"):
+        d = tmp_path / root / "images" / "moving_traps" / "walk"
+        d.mkdir(parents=True)
+        for i, f in enumerate(frames):
+            Image.fromarray(f).save(d / f"{i}.png")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.chdir(tmp_path / "one")
+    monkeypatch.delenv("SLM_GPUS", raising=False)
+    e1 = ghs.cli(["walk", "-v", "a", "-ct2pi", "255", "-loops", "6", "-p"], plot=False)
+    monkeypatch.chdir(tmp_path / "multi")
+    monkeypatch.setenv("SLM_GPUS", "0,0")
+    assert ghs.multi_devices(1) == [0, 0]
+    e2 = ghs.cli(["walk", "-v", "a", "-ct2pi", "255", "-loops", "6", "-p"], plot=False)
+    assert e1 == e2
+    for i in range(5):
+        for sub in (("holograms", "walk_a_holograms", f"{i}.npy"),):
+            a = np.load(tmp_path.joinpath("one", *sub))
+            b = np.load(tmp_path.joinpath("multi", *sub))
+            np.testing.assert_array_equal(a, b)
+        pa = np.array(Image.open(tmp_path / "one" / "images" / "moving_traps" / "walk_a_preview" / f"{i}.png"))
+        pb = np.array(Image.open(tmp_path / "multi" / "images" / "moving_traps" / "walk_a_preview" / f"{i}.png"))
+        np.testing.assert_array_equal(pa, pb)
