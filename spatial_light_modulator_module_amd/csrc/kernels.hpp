@@ -796,7 +796,9 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
                 const S a = ain_at(l, m);
                 const C g = mk<C>(z.x * inv_s * a, z.y * inv_s * a);
                 const long long idx = boff + PY * l + m * bstep;
-                C x = from_c64<C>(p.field_src[idx]);  // (loaded here: a prefetch at tile start measured no faster)
+                // loaded here: fetching the field with the tile's inputs measured slower
+                // (GD 1024^2 row pass 10.40 -> 10.89 us, same box, gpurun_out/s11)
+                C x = from_c64<C>(p.field_src[idx]);
                 const S ax2 = x.x * x.x + x.y * x.y;
                 const S inv = rsqrt_nr(ax2);
                 const S inv3 = inv * inv * inv;

@@ -45,8 +45,8 @@ ColFn col_table_cw(int mode, int tt) {
                 return u8 ? col_kernel<N, CW, COL_GD_STATS, TGT_U8, P, LID> : col_kernel<N, CW, COL_GD_STATS, TGT_F32, P, LID>;
             case COL_GD_GRAD:
                 return u8 ? col_kernel<N, CW, COL_GD_GRAD, TGT_U8, P, LID> : col_kernel<N, CW, COL_GD_GRAD, TGT_F32, P, LID>;
-            case COL_GD_FUSED:  // float32 GD on the default layout pair only (the 1-launch GD column side)
-                if constexpr (P == PREC_F32 && LID == LAYOUT_DEFAULT)
+            case COL_GD_FUSED:  // float32 GD only (the 1-launch GD column side)
+                if constexpr (P == PREC_F32)
                     return u8 ? col_kernel<N, CW, COL_GD_FUSED, TGT_U8, P, LID> : col_kernel<N, CW, COL_GD_FUSED, TGT_F32, P, LID>;
                 else
                     return nullptr;

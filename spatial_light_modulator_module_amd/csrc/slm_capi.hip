@@ -389,14 +389,18 @@ int configure(slm_plan* p, int prec) {
         HIP_TRY(hipGraphExecDestroy(p->gexec));
         p->gexec = nullptr;
     }
-    // layout pair: the narrow one for GS where both transforms have kernels
-    // for it ($SLM_LAYOUT=default forces the default pair). GD keeps the
-    // default: its field round trip through the row pass and its statistics
-    // pass measured slower on the narrow pair (1024^2: 28.9 -> 29.4 us per
-    // iteration, GS 20.9 -> 19.6 us). Device buffers are laid out at upload,
-    // so a plan keeps the pair it was created with.
+    // layout pair: the narrow one where both transforms have kernels for it
+    // ($SLM_LAYOUT=default forces the default pair; GS 1024^2 20.9 -> 19.6 us
+    // per iteration at r02). Device buffers are laid out at upload, so a plan
+    // keeps the pair it was created with.
     int lid = LAYOUT_DEFAULT;
-    const bool narrow_ok = p->algo == SLM_ALGO_GS && row_fn(row_key, ROW_GS_MAIN, prec, LAYOUT_NARROW) &&
+    // GD takes the narrow pair too since its column side became one launch
+    // (GD 1024^2 fused column pass 14.55 -> 13.66 us, 25.97 -> 25.19 us per
+    // iteration, bitwise the same phases: gpurun_out/s11; $SLM_GD_LAYOUT=default
+    // keeps the default pair for GD only)
+    const char* gl = std::getenv("SLM_GD_LAYOUT");
+    const bool algo_ok = p->algo == SLM_ALGO_GS || !(gl && !std::strcmp(gl, "default"));
+    const bool narrow_ok = algo_ok && row_fn(row_key, ROW_GS_MAIN, prec, LAYOUT_NARROW) &&
                            col_fn(col_key, cw, COL_GS_MAIN, TGT_F32, prec, LAYOUT_NARROW);
     const char* ls = std::getenv("SLM_LAYOUT");
     if (narrow_ok && !(ls && !std::strcmp(ls, "default"))) lid = LAYOUT_NARROW;
