@@ -40,12 +40,14 @@ def _close_frames(got, want):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("gif_type", ["h", "i"])
-def test_gd_gif_frames_vs_oracle(gpu, tmp_path, gif_type):
+@pytest.mark.parametrize("gif_type,n", [("h", 64), ("i", 64), ("h", 1024)])
+def test_gd_gif_frames_vs_oracle(gpu, tmp_path, gif_type, n):
+    """n = 1024 runs the chunks on the configs[2] plan (narrow layout pair:
+    the field read back and set again through that layout's relayouts)."""
     from spatial_light_modulator_module_amd.algorithms import gradient_descent
 
     rng = np.random.default_rng(4)
-    t = rng.uniform(0, 255, (64, 64)).astype(np.float32)
+    t = rng.uniform(0, 255, (n, n)).astype(np.float32)
     a = _args(tmp_path, gif_type=gif_type, unsettle=1)
     holo, out, err = gradient_descent(t, a)
     assert len(err) == 7

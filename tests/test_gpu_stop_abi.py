@@ -35,11 +35,14 @@ def _tol_between(err, s):
 
 
 @pytest.mark.gpu
-def test_gd_tolerance_stop_at_odd_iteration(gpu):
+@pytest.mark.parametrize("n", [64, 1024])
+def test_gd_tolerance_stop_at_odd_iteration(gpu, n):
+    """n = 1024: the configs[2] plan (narrow layout pair; a checked run takes
+    the two-launch column side, an unchecked one the fused side)."""
     from spatial_light_modulator_module_amd.algorithms import gradient_descent
 
     rng = np.random.default_rng(21)
-    t = rng.uniform(0, 255, (64, 64)).astype(np.float32)
+    t = rng.uniform(0, 255, (n, n)).astype(np.float32)
     _, _, err_full, _ = orc.gradient_descent_faithful(t, 12, 0.005, 1.0, 0, random_seed=5)
     tol = _tol_between(err_full, 5)  # stops after iteration index 5 (odd): 6 iterations
     ph_o, out_o, err_o, _ = orc.gradient_descent_faithful(t, 12, 0.005, 1.0, 0, tolerance=tol, random_seed=5)
