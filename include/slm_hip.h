@@ -125,6 +125,11 @@ int slm_plan_info(slm_plan* plan, int* info);
 /* panel widths (log2) of the plan's two blocked device layouts: X (row-pass
  * output, column-pass input, target) and Y (column-pass output, GD field) */
 int slm_plan_layout(slm_plan* plan, int* x_log2, int* y_log2);
+/* transform engine of the GS iteration kernels: 0 = Stockham pair (LDS
+ * exchange before every pass), 1 = wave-shuffle pair (fft_shuffle.hpp: 1024-
+ * point lines, float32; v_permlane swaps for four of the six exchanges; the
+ * GS and GD iteration kernels) */
+int slm_plan_engine(slm_plan* plan, int* col_engine, int* row_engine);
 
 /* Diagnostics: per-workgroup phase timestamps (s_memrealtime, 100 MHz: tile
  * start, loads complete, transforms done, stores complete, kernel entry) plus

@@ -73,6 +73,7 @@ _SIGNATURES = [
     ("slm_plan_kernel_bytes", ctypes.c_longlong, [_vp, _c_int]),
     ("slm_plan_info", _c_int, [_vp, _vp]),
     ("slm_plan_layout", _c_int, [_vp, _vp, _vp]),
+    ("slm_plan_engine", _c_int, [_vp, _vp, _vp]),
     ("slm_plan_read_trace", _c_int, [_vp, _c_int, _vp]),
     ("slm_gs", _c_int, [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_double, _vp, _vp, _vp, _vp, _vp]),
     ("slm_gd", _c_int,
@@ -281,7 +282,15 @@ class Plan:
         return {"col_cw": int(a[0]), "col_workgroups": int(a[1]), "col_threads": int(a[2]),
                 "row_threads": int(a[3]), "rows_per_workgroup": int(a[4]), "row_plan": int(a[5]),
                 "col_plan": int(a[6]), "precision": "f64" if a[7] == PRECISION_F64 else "f32",
-                "layout": self.layout()}
+                "layout": self.layout(), "engine": self.engine()}
+
+    def engine(self) -> tuple[str, str]:
+        """(column, row) transform engine of the GS iteration kernels:
+        "stockham" or "shuffle" (wave-shuffle pair, fft_shuffle.hpp)."""
+        c, r = ctypes.c_int(), ctypes.c_int()
+        check(self._lib.slm_plan_engine(self.handle, ctypes.byref(c), ctypes.byref(r)), "slm_plan_engine")
+        names = ("stockham", "shuffle")
+        return names[c.value], names[r.value]
 
     def layout(self) -> tuple[int, int]:
         """(X, Y) panel widths of the plan's blocked device layouts."""

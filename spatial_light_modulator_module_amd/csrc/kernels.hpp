@@ -25,6 +25,7 @@
 #include <type_traits>
 
 #include "fft_core.hpp"
+#include "fft_shuffle.hpp"
 
 namespace slm {
 
@@ -657,6 +658,16 @@ __device__ __forceinline__ void tile_loop(long long total, LoadF&& load, ProcF&&
 template <int K, bool COL>
 constexpr bool kLdsDouble = SLM_LDS_DOUBLE && K == 11;
 
+// Wave-shuffle transform pair (fft_shuffle.hpp) for the float32 GS iteration
+// on 1024-point narrow lines (plan key 11, the headline 1024^2 image): two of
+// the pair's six exchanges go through LDS, four are v_permlane swaps.
+// -DSLM_SHUFFLE=0 keeps the Stockham pair there (A/B builds).
+#ifndef SLM_SHUFFLE
+#define SLM_SHUFFLE 1
+#endif
+template <int K, int P>
+constexpr bool kShuffle = SLM_SHUFFLE && P == PREC_F32 && PlanOf<K>::N == kShufN && PlanOf<K>::E == 8;
+
 template <int K, int P>
 constexpr int row_wpe() {
     using X = XchgOf<P, (long long)RowCfg<K>::RPW * PlanOf<K>::ROWSTRIDE, K>;
@@ -693,8 +704,14 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
     // thread carries rows lrow * L + l, l < L.
     constexpr int QR = RowCfg<K>::QR;
     constexpr bool WV = RowCfg<K>::kWave;
+    // wave-shuffle pair: lane bit 0 selects the row of the pair, t per fft_shuffle.hpp
+    constexpr bool SHUF =
+        kShuffle<K, P> && (MODE == ROW_GS_MAIN || MODE == ROW_GD_MAIN || MODE == ROW_GD_LIN) && RPW == 2 && L == 1;
     int t, lrow;
-    if constexpr (RowCfg<K>::kRemap) {  // wave-line: T consecutive lanes per row, rows never cross a wave
+    if constexpr (SHUF) {
+        t = shuffle_t(threadIdx.x);
+        lrow = threadIdx.x & 1;
+    } else if constexpr (RowCfg<K>::kRemap) {  // wave-line: T consecutive lanes per row, rows never cross a wave
         t = threadIdx.x % T;
         lrow = threadIdx.x / T;
     } else {
@@ -710,7 +727,13 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
     if constexpr (MODE == ROW_GS_MAIN || MODE == ROW_GD_MAIN || MODE == ROW_GD_LIN) trace_entry(p.trace);
     sgpr_pin(p.in, p.out, p.holo, p.H, p.B, p.ntile, p.tw, p.ain, p.wt, gridDim.x);
     Twiddles<K, C, tw_mode<P, RowCfg<K>::THREADS, K, false>()> tw;
-    load_twiddles<K, C>(tw, t, p.tw);
+    static_assert(!SHUF || (std::is_same_v<X, float2> && sizeof(smem) >= 4 * kShufN * sizeof(float2)),
+                  "the shuffle pair needs two 2-line complex64 exchange buffers");
+    ShuffleTw stw;
+    if constexpr (SHUF)
+        load_shuffle_tw(stw, threadIdx.x, static_cast<const float2*>(p.tw) + twiddle_count_key(K));
+    else
+        load_twiddles<K, C>(tw, t, p.tw);
 
     // tile = (hologram b, row group g); rows g * RPW + lrow + l. Inputs (Y,
     // the GD field) are in layout Y, outputs (X) in layout X; row l + 1 sits
@@ -779,7 +802,11 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
             fft_line<K, false, C>(v, t, tw, lds);
         } else if constexpr (MODE == ROW_GS_MAIN) {
             // A -> B = a_in A/|A| (src/algorithms.py:30)
-            fft_pair<K, true, false, C>(v, t, tw, lds, [&](int l, int m, C& z) { z = unit_scale(z, ain_at(l, m)); });
+            auto epi = [&](int l, int m, C& z) { z = unit_scale(z, ain_at(l, m)); };
+            if constexpr (SHUF)
+                shuffle_pair<true, false>(v[0], threadIdx.x, stw, reinterpret_cast<float2*>(smem), epi);
+            else
+                fft_pair<K, true, false, C>(v, t, tw, lds, epi);
         } else if constexpr (MODE == ROW_GD_INIT_Y) {
             fft_pair<K, true, false, C>(v, t, tw, lds, [&](int l, int m, C& z) {
                 const S a = ain_at(l, m);
@@ -792,7 +819,7 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
             // input -= lr * dEdX (:91); next forward input x/|x| a_in (:84).
             const S lr = (S)p.lr[p.iter];
             const S inv_s = (S)1 / (S)p.holo;
-            fft_pair<K, true, false, C>(v, t, tw, lds, [&](int l, int m, C& z) {
+            auto epi = [&](int l, int m, C& z) {
                 const S a = ain_at(l, m);
                 const C g = mk<C>(z.x * inv_s * a, z.y * inv_s * a);
                 const long long idx = boff + PY * l + m * bstep;
@@ -810,7 +837,11 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
                 const float2 xs = to_c64(x);  // the field is stored in complex64
                 p.field[idx] = xs;
                 z = normalize(from_c64<C>(xs), a);
-            });
+            };
+            if constexpr (SHUF)
+                shuffle_pair<true, false>(v[0], threadIdx.x, stw, reinterpret_cast<float2*>(smem), epi);
+            else
+                fft_pair<K, true, false, C>(v, t, tw, lds, epi);
         } else if constexpr (MODE == ROW_GD_LIN) {
             // The column pass left U = ifft_col(mask F P) and V = ifft_col(mask F T);
             // ifft_col(mask F (s P - T)) = s U - V with s = norm / max |F|^2 of this
@@ -844,7 +875,7 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
                 }
             const S lr = (S)p.lr[p.iter];
             const S inv_s = (S)1 / (S)p.holo;
-            fft_pair<K, true, false, C>(v, t, tw, lds, [&](int l, int m, C& z) {
+            auto epi = [&](int l, int m, C& z) {
                 // dEdF = ifft2(...) * a_in (:87-89); dEdX_complex (:179-185); x -= lr dEdX (:91)
                 const S a = ain_at(l, m);
                 const C g = mk<C>(z.x * inv_s * a, z.y * inv_s * a);
@@ -860,7 +891,11 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
                 const float2 xs = to_c64(x);
                 p.field[boff + PY * l + m * bstep] = xs;
                 z = normalize(from_c64<C>(xs), a);
-            });
+            };
+            if constexpr (SHUF)
+                shuffle_pair<true, false>(v[0], threadIdx.x, stw, reinterpret_cast<float2*>(smem), epi);
+            else
+                fft_pair<K, true, false, C>(v, t, tw, lds, epi);
         }
         trace_point(trace, tile, 2, false);
         if (p.wt) {  // uniform: one branch per tile, not per store
@@ -992,8 +1027,13 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P, M
 
     // a thread carries columns c .. c + L - 1 of the tile (adjacent in the
     // blocked layout: one 16-B access for L = 2)
+    // wave-shuffle pair: lane bit 0 selects the column (as here), t per fft_shuffle.hpp
+    // (the GS and GD iteration modes)
+    constexpr bool SHUF = kShuffle<K, P> && CW == 2 && L == 1 &&
+                          (MODE == COL_GS_MAIN || MODE == COL_GD_STATS || MODE == COL_GD_GRAD ||
+                           MODE == COL_GD_FUSED || MODE == COL_GD_LIN);
     const int c = (threadIdx.x % (CW / L)) * L;
-    const int t = threadIdx.x / (CW / L);
+    const int t = SHUF ? shuffle_t(threadIdx.x) : threadIdx.x / (CW / L);
     // inputs (X, target) in layout X, outputs (Y) in layout Y: row y = t + T m
     constexpr long long kStep = (long long)kPanelOf<LAYOUT_X> * T;
     constexpr long long kStepY = (long long)kPanelOf<LAYOUT_Y> * T;
@@ -1009,7 +1049,13 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P, M
         trace_entry(p.trace);
     sgpr_pin(p.in, p.out, p.tgt, p.holo, p.nwg, p.B, p.tw, p.checked, p.wt, gridDim.x);
     Twiddles<K, C, tw_mode<P, THREADS, K, true, L>()> tw;
-    load_twiddles<K, C>(tw, t, p.tw);
+    static_assert(!SHUF || (std::is_same_v<X, float2> && sizeof(smem) >= 4 * kShufN * sizeof(float2)),
+                  "the shuffle pair needs two 2-line complex64 exchange buffers");
+    ShuffleTw stw;
+    if constexpr (SHUF)
+        load_shuffle_tw(stw, threadIdx.x, static_cast<const float2*>(p.tw) + twiddle_count_key(K));
+    else
+        load_twiddles<K, C>(tw, t, p.tw);
     constexpr bool kTarget = (MODE == COL_GS_MAIN || MODE == COL_GD_STATS || MODE == COL_GD_GRAD ||
                               MODE == COL_GD_FUSED || MODE == COL_GD_LIN);
     constexpr int NT = kTarget ? E : 1;
@@ -1136,16 +1182,30 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P, M
             // Both terms are inverse-transformed along the columns here (Y, Y2); the row
             // pass forms s U - V once every column workgroup's max is in memory.
             double mx = 0.0, s2 = 0.0, st = 0.0;
-            fft_line_epi<K, false, C>(v, t, tw, lds, [&](int l, int m, C& z) {
+            auto stats = [&](int l, int m, C& z) {
                 const double ed = (double)(float)(z.x * z.x + z.y * z.y);
                 mx = fmax(mx, ed);
                 s2 += ed * ed;
                 st += ed * (double)tv[l][m];
-            });
+            };
+            if constexpr (SHUF) {
+                shuffle_first<false>(v[0], threadIdx.x, stw, reinterpret_cast<float2*>(smem));
+                static_for<E>([&](auto mc) { stats(0, decltype(mc)::value, v[0][decltype(mc)::value]); });
+            } else {
+                fft_line_epi<K, false, C>(v, t, tw, lds, stats);
+            }
             trace_point(trace, tile, 2, false);
             V wu[L][E], wv[L][E];
             gd_split_terms<C>(v, tv, (S)p.wa, wu, wv);
-            gd_inverse_pair<K, C, LW == 2 * CW>(wu, wv, t, tw, lds, smem, c);
+            if constexpr (SHUF) {
+                // U then V: V's exchange reuses the first transform's buffer, which
+                // every wave left before U's barrier
+                float2* const buf = reinterpret_cast<float2*>(smem);
+                shuffle_second<true>(wu[0], threadIdx.x, stw, buf + 2 * kShufN);
+                shuffle_second<true>(wv[0], threadIdx.x, stw, buf);
+            } else {
+                gd_inverse_pair<K, C, LW == 2 * CW>(wu, wv, t, tw, lds, smem, c);
+            }
             const long long ob = out_base(b, wg);
             st_tile_to(p.out, ob, wu);
             st_tile_to(p.out2, ob, wv);
@@ -1168,12 +1228,18 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P, M
             // registers across the barrier instead of being recomputed by a
             // second launch (COL_GD_STATS + COL_GD_GRAD).
             double mx = 0.0, s2 = 0.0, st = 0.0;
-            fft_line_epi<K, false, C>(v, t, tw, lds, [&](int l, int m, C& z) {
+            auto stats = [&](int l, int m, C& z) {
                 const double ed = (double)(float)(z.x * z.x + z.y * z.y);
                 mx = fmax(mx, ed);
                 s2 += ed * ed;
                 st += ed * (double)tv[l][m];
-            });
+            };
+            if constexpr (SHUF) {
+                shuffle_first<false>(v[0], threadIdx.x, stw, reinterpret_cast<float2*>(smem));
+                static_for<E>([&](auto mc) { stats(0, decltype(mc)::value, v[0][decltype(mc)::value]); });
+            } else {
+                fft_line_epi<K, false, C>(v, t, tw, lds, stats);
+            }
             trace_point(trace, tile, 2, false);
             block_reduce_stats<THREADS>(mx, s2, st);
             if (threadIdx.x == 0) {  // the statistics partials (folded after the run by stats_reduce_kernel)
@@ -1200,7 +1266,10 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P, M
                     const S w = ((S)1 + (S)p.wa * (S)tl / (S)255) * (o - (S)tl);
                     v[l][mm] = cv<V>(mk<C>(z.x * w, z.y * w));
                 }
-            fft_line<K, true, C>(v, t, tw, lds);
+            if constexpr (SHUF)
+                shuffle_second<true>(v[0], threadIdx.x, stw, reinterpret_cast<float2*>(smem) + 2 * kShufN);
+            else
+                fft_line<K, true, C>(v, t, tw, lds);
             st_tile(out_base(b, wg), v);
             return;
         } else {
@@ -1229,8 +1298,13 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P, M
             // pass and reading it back measured slower at 1024^2 (8.9 + 9.5 us
             // against 5.7 + 10.9 us per iteration: the extra store tail costs
             // more than the forward transform saves)
-            if constexpr (MODE == COL_GD_STATS)
+            if constexpr (MODE == COL_GD_STATS && SHUF) {
+                shuffle_first<false>(v[0], threadIdx.x, stw, reinterpret_cast<float2*>(smem));
+                static_for<E>([&](auto mc) { epi(0, decltype(mc)::value, v[0][decltype(mc)::value]); });
+            } else if constexpr (MODE == COL_GD_STATS)
                 fft_line_epi<K, false, C>(v, t, tw, lds, epi);
+            else if constexpr (SHUF)
+                shuffle_pair<false, true>(v[0], threadIdx.x, stw, reinterpret_cast<float2*>(smem), epi);
             else
                 fft_pair<K, false, true, C>(v, t, tw, lds, epi);
             trace_point(trace, tile, 2, false);

@@ -126,6 +126,15 @@ int get_twiddles(int pk, int prec, const void** out) {
         host.push_back(1.0);
         host.push_back(0.0);
     }
+    if (pl.n == kShufN && pl.e == 8) {
+        // the wave-shuffle pair's table (fft_shuffle.hpp): the N roots
+        // exp(-2 pi i e / N), after the Stockham entries (twiddle_count_key)
+        for (int e = 0; e < pl.n; ++e) {
+            const double ang = -2.0 * M_PI * (double)e / (double)pl.n;
+            host.push_back(std::cos(ang));
+            host.push_back(std::sin(ang));
+        }
+    }
     void* d = nullptr;
     if (prec == PREC_F64) {
         HIP_TRY(hipMalloc(&d, host.size() * sizeof(double)));
@@ -1190,6 +1199,17 @@ int slm_plan_info(slm_plan* p, int* info) {
     info[5] = p->row_key;
     info[6] = p->col_key;
     info[7] = p->prec;
+    return 0;
+}
+
+int slm_plan_engine(slm_plan* p, int* col_engine, int* row_engine) {
+    if (!p || !col_engine || !row_engine) return fail(SLM_ERR_ARG, "null argument");
+    // mirrors kernels.hpp: kShuffle<K, P> && (CW == 2 | RPW == 2) && one line per thread
+    auto shuf = [&](int key) {
+        return SLM_SHUFFLE && p->prec == PREC_F32 && key >= 0 && kPlans[key].n == kShufN && kPlans[key].e == 8;
+    };
+    *col_engine = shuf(p->col_key) && p->cw == 2 ? 1 : 0;
+    *row_engine = shuf(p->row_key) && p->rpw == 2 ? 1 : 0;
     return 0;
 }
 

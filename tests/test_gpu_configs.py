@@ -270,11 +270,13 @@ def test_gd_fused_column_pass(gpu, shape, u8):
     hologram's max, combine) against the two-launch path (SLM_GD_MODE=two:
     statistics pass, then a gradient pass that recomputes F and forms G
     before its inverse) and the split path with no in-launch wait
-    (SLM_GD_MODE=lin). The split moves the subtraction behind the inverse
-    transform, so phases agree to float32 rounding (< 5e-6 rad rms after 60
-    iterations), not bitwise; graph-replayed and timed (direct) fused runs are
-    bitwise equal, and the timed run shows one column launch per iteration and
-    no statistics launches. Hologram 0 is also held to the float64 oracle."""
+    (SLM_GD_MODE=lin). Fused and two-launch phases are bitwise equal. The
+    split moves the subtraction behind the inverse transform, so it agrees to
+    float32 rounding (2.6e-6 - 5.1e-6 rad rms after 60 iterations), not
+    bitwise; graph-replayed and timed (direct) fused runs are bitwise equal,
+    and the timed run shows one column launch per iteration and no statistics
+    launches. Hologram 0 of the fused and the split runs is also held to the
+    float64 oracle."""
     from spatial_light_modulator_module_amd import _lib
     from spatial_light_modulator_module_amd import algorithms as alg
 
@@ -297,19 +299,21 @@ def test_gd_fused_column_pass(gpu, shape, u8):
     assert two[3][_lib.KERNEL_GD_STATS] == loops and two[3][_lib.KERNEL_COL_MAIN] == loops
     assert lin[3][_lib.KERNEL_GD_STATS] == 0 and lin[3][_lib.KERNEL_COL_MAIN] == loops
     for k in range(b):
-        for name, other in (("two-launch", two), ("split, no wait", lin)):
-            rms = orc.phase_rms(fused[0][k], other[0][k])
-            print(f"[parity] GD fused vs {name} {shape} hologram {k}: phase rms {rms:.3e}")
-            assert rms < 5e-6
+        # same transforms and gradient arithmetic: bitwise
+        np.testing.assert_array_equal(fused[0][k], two[0][k])
+        rms = orc.phase_rms(fused[0][k], lin[0][k])
+        print(f"[parity] GD fused vs split, no wait {shape} hologram {k}: phase rms {rms:.3e}")
+        assert rms < PHASE_RMS_TOL  # two float32 roundings of the same iteration, each held to the oracle below
         np.testing.assert_array_equal(fused[0][k], fused_t[0][k])
     for other, rtol in ((two, 1e-5), (lin, 1e-4)):  # the split path rounds differently (s U - V after the inverse)
         np.testing.assert_allclose(fused[2][..., 3], other[2][..., 3], rtol=rtol)
         np.testing.assert_allclose(fused[1], other[1], rtol=1e-3, atol=1e-3 * float(np.max(other[1])))
     ref, _, ref_err, _ = fast_f64.gradient_descent_f64(t[0].astype(np.float64) if u8 else t[0], loops, 0.005, 1.0,
                                                         initial_field=x0[0])
-    rms = orc.phase_rms(fused[0][0], ref)
-    print(f"[parity] GD fused {shape} hologram 0 vs float64 oracle, {loops} iterations: phase rms {rms:.3e}")
-    assert rms < PHASE_RMS_TOL
+    for name, res in (("fused", fused), ("split", lin)):
+        rms = orc.phase_rms(res[0][0], ref)
+        print(f"[parity] GD {name} {shape} hologram 0 vs float64 oracle, {loops} iterations: phase rms {rms:.3e}")
+        assert rms < PHASE_RMS_TOL
 
 
 @pytest.mark.gpu

@@ -57,7 +57,8 @@ def test_warm_start_parity_large(gpu, n, span, u8):
     configs[1]): its plan must be the one bench.py times -- narrow 1024 plan
     (key 11) on both axes, 2-column tiles, the narrow layout pair (8-wide X,
     2-wide Y panels), i.e. col_kernel<11, 2, GS_MAIN, f32 target, f32, narrow>
-    -- so the gate covers the exact instantiation the roofline is quoted on."""
+    -- on the wave-shuffle transform pair (fft_shuffle.hpp) in both kernels,
+    so the gate covers the exact instantiation the roofline is quoted on."""
     rng = np.random.default_rng(n)
     t = rng.integers(0, 256, (n, n)).astype(np.uint8) if u8 else rng.uniform(0, 255, (n, n)).astype(np.float32)
     with sfft.set_workers(WORKERS):
@@ -66,8 +67,8 @@ def test_warm_start_parity_large(gpu, n, span, u8):
     if n == 1024 and not u8:
         with gpu.Plan(gpu.ALGO_GS, 1, n, n, gpu.TGT_F32, False, span) as p:
             info = p.info()
-        assert (info["row_plan"], info["col_plan"], info["col_cw"], info["layout"], info["precision"]) == \
-            (11, 11, 2, (8, 2), "f32"), info
+        assert (info["row_plan"], info["col_plan"], info["col_cw"], info["layout"], info["precision"],
+                info["engine"]) == (11, 11, 2, (8, 2), "f32", ("shuffle", "shuffle")), info
     for prec, precision in (("f64", gpu.PRECISION_F64), ("f32", gpu.PRECISION_F32)):
         ph, err = _gpu_warm_run(gpu, t, phi_w, span, precision)
         rms = orc.phase_rms(ph, ref)
