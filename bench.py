@@ -257,7 +257,7 @@ def main():
 
     def step():
         plan.run(iters)
-        plan.gather_phase(counts, root=0)  # synchronises the plan stream
+        plan.gather_phase(counts, root=0)  # device-side gather, stream-ordered (no host sync per step)
 
     for _ in range(opt.warmup):
         step()

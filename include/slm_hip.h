@@ -168,8 +168,9 @@ int slm_comm_destroy(void);
 /* Gather every rank's phase output to `root`: rank r contributes its plan's
  * batch (counts[r] holograms, same h x w everywhere); on root, host_out
  * receives sum(counts) x h x w float32 in rank order (may be NULL to leave
- * the gathered array on the device). Collective; enqueued on the plan stream
- * and synchronised before returning. */
+ * the gathered array on the device). Collective; enqueued on the plan stream,
+ * which is synchronised before returning only when host_out is given (a
+ * device-side gather stays stream-ordered with the plan's later work). */
 int slm_plan_gather_phase(slm_plan* plan, const int* counts, int root, float* host_out);
 /* The same collective for the per-iteration statistics that become each
  * hologram's error_evolution (src/generate_hologram_sequence.py:19-31 keeps one

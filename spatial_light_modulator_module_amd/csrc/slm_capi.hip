@@ -1455,12 +1455,15 @@ int gather_slab(slm_plan* p, const void* src, long long per_item, size_t elem, n
             }
         }
         if (n > 1) NCCL_TRY(ncclGroupEnd());
-        HIP_TRY(hipStreamSynchronize(p->stream));
-        if (host_out && elems) RC(copy_sync(host_out, dst, (size_t)elems * elem, hipMemcpyDeviceToHost, p->stream));
+        // a device-side gather stays stream-ordered (the next run on this
+        // stream, a read or slm_plan_sync wait for it); a host copy waits here
+        if (host_out && elems) {
+            HIP_TRY(hipStreamSynchronize(p->stream));
+            RC(copy_sync(host_out, dst, (size_t)elems * elem, hipMemcpyDeviceToHost, p->stream));
+        }
     } else {
         if (!g_comm) return fail(SLM_ERR_COMM, "no communicator");
         if (p->B) NCCL_TRY(ncclSend(src, (size_t)p->B * per_item, dt, root, g_comm, p->stream));
-        HIP_TRY(hipStreamSynchronize(p->stream));
     }
     return 0;
 }
