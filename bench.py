@@ -317,6 +317,15 @@ def main():
                               "frac_model": round(68 * bper * n * n / iter_s / 1e9 / HBM_PEAK_GBS, 4),
                               "frac_physical": round(36 * bper * n * n / iter_s / 1e9 / HBM_PEAK_GBS, 4)},
                 "kernels": {k: {kk: _round(vv) for kk, vv in v.items()} for k, v in rows.items()}}
+    # measured streaming-copy rates: HBM-sized buffers, and buffers
+    # the size of this loop's working set (field X + Y + target), which the
+    # 256 MiB Infinity Cache holds between launches
+    work = (8 + 8 + 4) * bper * n * n
+    copy = {"hbm_1gib_gbs": round(_lib.copy_bandwidth(1 << 30, 10), 1),
+            "working_set_gbs": round(_lib.copy_bandwidth(work // 2, 50), 1), "working_set_bytes": work}
+    copy["dominant_frac_of_copy_hbm"] = round(dr["achieved_gbs"] / copy["hbm_1gib_gbs"], 4)
+    copy["dominant_physical_frac_of_copy_working_set"] = round(dr["physical_gbs"] / copy["working_set_gbs"], 4)
+    roofline["measured_copy"] = copy
     out = {
         "metric": METRIC, "value": round(value, 3), "unit": "holograms/s", "n_gpus": world,
         "steps": opt.steps, "warmup": opt.warmup, "ms_per_step": round(ms_per_step, 4),

@@ -63,6 +63,11 @@ int slm_device_count(void);
 const char* slm_last_error(void);
 const char* slm_version(void);
 int slm_supported_length(int n);    /* 1 if n is a supported row/column length */
+/* Measured streaming-copy rate (read + write bytes / s, in GB/s) of two
+ * `bytes`-sized device buffers on the current device, `reps` timed copies
+ * (16 B per lane, grid-stride): the practical peak next to the 8 TB/s spec
+ * (SURVEY.md 8d asks for a measured copy-kernel peak). */
+int slm_copy_bandwidth(long long bytes, int reps, double* gbs);
 
 /* ---- plans: device-resident batches ------------------------------------
  * A plan holds `batch` holograms of height x width on the current device.

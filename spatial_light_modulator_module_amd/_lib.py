@@ -53,6 +53,7 @@ _SIGNATURES = [
     ("slm_last_error", ctypes.c_char_p, []),
     ("slm_version", ctypes.c_char_p, []),
     ("slm_supported_length", _c_int, [_c_int]),
+    ("slm_copy_bandwidth", _c_int, [ctypes.c_longlong, _c_int, _P(_c_double)]),
     ("slm_plan_create", _c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _P(_vp)]),
     ("slm_plan_destroy", _c_int, [_vp]),
     ("slm_plan_set_target", _c_int, [_vp, _vp]),
@@ -157,6 +158,15 @@ def init(device: int | None = None) -> None:
 
 def device_count() -> int:
     return int(load().slm_device_count())
+
+
+def copy_bandwidth(nbytes: int, reps: int = 20) -> float:
+    """Measured streaming-copy rate of two nbytes device buffers, GB/s
+    (read + write; slm_copy_bandwidth)."""
+    init()
+    g = ctypes.c_double()
+    check(load().slm_copy_bandwidth(int(nbytes), int(reps), ctypes.byref(g)), "slm_copy_bandwidth")
+    return float(g.value)
 
 
 class Plan:

@@ -153,6 +153,24 @@ __global__ void fill_int_kernel(int* p, int n, int v) {
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = v;
 }
 
+// Streaming copy, 16 B per lane, four non-temporal loads in flight per lane
+// before their stores, grid-stride (slm_copy_bandwidth): the practical HBM /
+// Infinity-Cache rate the roofline fractions are read against.
+typedef float v4f __attribute__((ext_vector_type(4)));
+__global__ void __launch_bounds__(256) copy_f4_kernel(const v4f* __restrict__ in, v4f* __restrict__ out,
+                                                      long long n) {
+    const long long stride = (long long)gridDim.x * 1024;
+    for (long long base = blockIdx.x * 1024LL + threadIdx.x; base < n; base += stride) {
+        v4f r[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (base + k * 256 < n) r[k] = __builtin_nontemporal_load(in + base + k * 256);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (base + k * 256 < n) __builtin_nontemporal_store(r[k], out + base + k * 256);
+    }
+}
+
 // max(T) and sum(T^2) per hologram in double (np.amax(demanded_output),
 // src/algorithms.py:23; sum(T^2) is the constant term of the error expansion).
 // Stage 1: ts_blocks(holo) workgroups per hologram, each thread reducing
@@ -811,6 +829,39 @@ int slm_device_count(void) {
 }
 
 const char* slm_last_error(void) { return g_err.c_str(); }
+
+int slm_copy_bandwidth(long long bytes, int reps, double* gbs) {
+    if (!gbs || bytes < 16 || reps < 1) return fail(SLM_ERR_ARG, "bad copy-bandwidth arguments");
+    RC(ensure_device());
+    const long long n = bytes / 16;
+    v4f *a = nullptr, *b = nullptr;
+    hipStream_t st = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int dev = 0, cus = 0, rc = 0;
+    auto hip = [&](hipError_t e) {
+        if (e != hipSuccess && !rc) rc = fail(SLM_ERR_HIP, "copy bandwidth: %s", hipGetErrorString(e));
+        return rc == 0;
+    };
+    if (hip(hipGetDevice(&dev)) && hip(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) &&
+        hip(hipMalloc(&a, n * 16)) && hip(hipMalloc(&b, n * 16)) && hip(hipStreamCreate(&st)) &&
+        hip(hipEventCreate(&e0)) && hip(hipEventCreate(&e1)) && hip(hipMemsetAsync(a, 1, n * 16, st)) &&
+        hip(hipMemsetAsync(b, 0, n * 16, st))) {
+        // enough workgroups that a working-set-sized copy still fills the chip
+        const int grid = (int)std::max<long long>(1, std::min<long long>((long long)cus * 32, (n + 1023) / 1024));
+        hipLaunchKernelGGL(copy_f4_kernel, dim3(grid), dim3(256), 0, st, a, b, n);  // warm-up
+        hip(hipEventRecord(e0, st));
+        for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(copy_f4_kernel, dim3(grid), dim3(256), 0, st, a, b, n);
+        float ms = 0.f;
+        if (hip(hipEventRecord(e1, st)) && hip(hipEventSynchronize(e1)) && hip(hipEventElapsedTime(&ms, e0, e1)))
+            *gbs = 2.0 * 16.0 * (double)n * reps / (ms * 1e-3) / 1e9;
+    }
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (st) (void)hipStreamDestroy(st);
+    if (a) (void)hipFree(a);
+    if (b) (void)hipFree(b);
+    return rc;
+}
 
 const char* slm_version(void) { return "libslm_hip 0.1 (gfx950)"; }
 
