@@ -55,14 +55,16 @@ def test_gd_tolerance_stop_at_odd_iteration(gpu, n):
 
 
 @pytest.mark.gpu
-def test_gs_batch_with_different_stop_iterations(gpu):
+@pytest.mark.parametrize("n", [128, 1024])
+def test_gs_batch_with_different_stop_iterations(gpu, n):
     """One tolerance, three holograms scaled so that each stops at a different
     iteration (2, 3 and 5): GS is scale free in the target, the error scales
-    with its square."""
+    with its square. n = 1024 runs the checked (early-exit) wave-shuffle
+    kernels: whole workgroups leave before the pair's barriers."""
     from spatial_light_modulator_module_amd import algorithms as alg
 
     rng = np.random.default_rng(33)
-    base = rng.uniform(0, 255, (128, 128))
+    base = rng.uniform(0, 255, (n, n))
     phi0 = rng.uniform(-np.pi, np.pi, base.shape).astype(np.float32)
     _, _, err_base = orc.gerchberg_saxton_faithful(base.astype(np.float32), 12, initial_phase=phi0)
     tol = 1000.0
