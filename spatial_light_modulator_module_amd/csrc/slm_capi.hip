@@ -783,6 +783,9 @@ int enqueue_run(slm_plan* p, int loops, double tol, int checked, float wa) {
 void free_plan(slm_plan* p) {
     if (!p) return;
     (void)hipSetDevice(p->device);
+    // work still queued on the plan stream (an unsynchronised run, a
+    // stream-ordered device gather or RCCL send) finishes before its buffers go
+    if (p->stream) (void)hipStreamSynchronize(p->stream);
     for (void* ptr : {(void*)p->xa, (void*)p->xb, (void*)p->y, (void*)p->field, p->tgt, (void*)p->ain,
                       (void*)p->phase_in, (void*)p->phase_out, (void*)p->e_out, (void*)p->partials,
                       (void*)p->stats, (void*)p->stop, (void*)p->norm, (void*)p->normf, (void*)p->sum_t2,
