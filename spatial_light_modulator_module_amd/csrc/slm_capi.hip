@@ -1451,6 +1451,8 @@ int slm_comm_init(int nranks, int rank, const unsigned char* id128) {
 
 int slm_comm_destroy(void) {
     if (g_comm) {
+        // device gathers return without waiting: let queued RCCL work finish first
+        (void)hipDeviceSynchronize();
         ncclCommDestroy(g_comm);
         g_comm = nullptr;
     }
