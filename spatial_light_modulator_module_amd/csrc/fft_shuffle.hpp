@@ -259,4 +259,157 @@ __device__ __forceinline__ void shuffle_pair(float2 (&v)[8], int tid, const Shuf
     shuffle_second<INV2>(v, tid, tw, lds + 2 * kShufN);
 }
 
+// ==========================================================================
+// 4096-point rows (one row per 256-thread workgroup, 16 slots per thread,
+// radices 16.16.16; tools/shuffle4096_model.py simulates the schedule):
+//
+//   A (load/store)  slots pos 8-11   lanes 0-5 = pos 0-5          waves = pos 6, 7
+//   P1 radix 16, twiddle w_4096^(t k1)
+//   X1 LDS (+ barrier)
+//   B               slots pos 4-7    lanes 1, 3, 4, 5 = pos 0-3   lanes 0, 2, waves = pos 8-11
+//   P2 radix 16, twiddle w_256^(n k2), n = pos 0-3
+//   X2 registers:   slot bit 0 <-> lane bit 1 (quad_perm), slot bit 1 <-> lane
+//                   bit 3 (row_ror:8 under bank masks), slot bit 2 <-> lane bit 4
+//                   (v_permlane16_swap), slot bit 3 <-> lane bit 5 (v_permlane32_swap)
+//   C               slots pos 0-3    lanes 1, 3, 4, 5 = pos 4-7
+//   P3 radix 16: slot m holds frequency klow(tid) + 256 m.
+// ==========================================================================
+constexpr int kShuf4N = 4096;
+
+__device__ __forceinline__ int lane_bit(int tid, int b) { return (tid >> b) & 1; }
+
+// frequency index (minus 256 m) of the element in slot m after the first transform
+__device__ __forceinline__ int shuffle4096_klow(int tid) {
+    const int w = tid >> 6;
+    return lane_bit(tid, 0) | (lane_bit(tid, 2) << 1) | ((w & 1) << 2) | (((w >> 1) & 1) << 3) |
+           (lane_bit(tid, 1) << 4) | (lane_bit(tid, 3) << 5) | (lane_bit(tid, 4) << 6) | (lane_bit(tid, 5) << 7);
+}
+
+struct ShuffleTw4096 {
+    float2 p1[15];  // w_4096^(t k1)
+    float2 p2[15];  // w_256^(n k2), n = lane bits 1, 3, 4, 5
+};
+
+__device__ __forceinline__ void load_shuffle4096_tw(ShuffleTw4096& tw, int tid, const float2* __restrict__ roots) {
+    const int n = lane_bit(tid, 1) | (lane_bit(tid, 3) << 1) | (lane_bit(tid, 4) << 2) | (lane_bit(tid, 5) << 3);
+    static_for<15>([&](auto kc) {
+        constexpr int k = decltype(kc)::value + 1;
+        tw.p1[k - 1] = roots[tid * k];
+        tw.p2[k - 1] = roots[16 * n * k];
+    });
+}
+
+__device__ __forceinline__ int shuffle4096_pos_b(int tid, int m) {
+    const int w = tid >> 6;
+    return lane_bit(tid, 1) | (lane_bit(tid, 3) << 1) | (lane_bit(tid, 4) << 2) | (lane_bit(tid, 5) << 3) | (m << 4) |
+           (lane_bit(tid, 0) << 8) | (lane_bit(tid, 2) << 9) | ((w & 1) << 10) | (((w >> 1) & 1) << 11);
+}
+// X1 slot map: p ^ H(p >> 8), H = j0 -> bit 3, j1 -> bits 2 and 4 (0 extra
+// LDS cycles for both directions' 16-lane writes and 32-lane reads)
+__device__ __forceinline__ int shuffle4096_slot(int p) {
+    const int j0 = (p >> 8) & 1, j1 = (p >> 9) & 1;
+    return p ^ ((j0 << 3) | (j1 << 2) | (j1 << 4));
+}
+template <bool A_TO_B>
+__device__ __forceinline__ void shuffle4096_x1(float2 (&v)[16], int tid, float2* buf) {
+    static_for<16>([&](auto mc) {
+        constexpr int m = decltype(mc)::value;
+        buf[shuffle4096_slot(A_TO_B ? (tid | (m << 8)) : shuffle4096_pos_b(tid, m))] = v[m];
+    });
+    lds_barrier();
+    static_for<16>([&](auto mc) {
+        constexpr int m = decltype(mc)::value;
+        v[m] = buf[shuffle4096_slot(A_TO_B ? shuffle4096_pos_b(tid, m) : (tid | (m << 8)))];
+    });
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float x) {
+    return as_f((unsigned)__builtin_amdgcn_update_dpp(0, (int)as_u(x), CTRL, 0xF, 0xF, false));
+}
+// slot pair (a: bit clear, c: bit set) <-> lane bit 1: partner lane = lane ^ 2 (quad_perm [2,3,0,1])
+__device__ __forceinline__ void swap_l1(float2& a, float2& c, int x) {
+    constexpr int kXor2 = 0x4E;
+    const float2 pa = make_float2(dpp_f32<kXor2>(a.x), dpp_f32<kXor2>(a.y));
+    const float2 pc = make_float2(dpp_f32<kXor2>(c.x), dpp_f32<kXor2>(c.y));
+    const float2 na = x ? pc : a;
+    const float2 nc = x ? c : pa;
+    a = na;
+    c = nc;
+}
+// slot pair <-> lane bit 3: partner lane = lane ^ 8 (row_ror:8); lanes with the
+// bit set (banks 2, 3) replace a, lanes with it clear (banks 0, 1) replace c
+__device__ __forceinline__ float dpp_ror8_banks(float old, float src, int banks_hi) {
+    return banks_hi ? as_f((unsigned)__builtin_amdgcn_update_dpp((int)as_u(old), (int)as_u(src), 0x128, 0xF, 0xC, false))
+                    : as_f((unsigned)__builtin_amdgcn_update_dpp((int)as_u(old), (int)as_u(src), 0x128, 0xF, 0x3, false));
+}
+__device__ __forceinline__ void swap_l3(float2& a, float2& c) {
+    const float2 na = make_float2(dpp_ror8_banks(a.x, c.x, 1), dpp_ror8_banks(a.y, c.y, 1));
+    const float2 nc = make_float2(dpp_ror8_banks(c.x, a.x, 0), dpp_ror8_banks(c.y, a.y, 0));
+    a = na;
+    c = nc;
+}
+// X2 (its own inverse): the four slot bits <-> lane bits 1, 3, 4, 5
+__device__ __forceinline__ void shuffle4096_x2(float2 (&v)[16], int tid) {
+    const int x1 = lane_bit(tid, 1);
+    static_for<8>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        constexpr int m = 2 * i;  // slot bit 0 clear
+        swap_l1(v[m], v[m | 1], x1);
+    });
+    static_for<8>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        constexpr int m = (i & 1) | ((i >> 1) << 2);  // slot bit 1 clear
+        swap_l3(v[m], v[m | 2]);
+    });
+    static_for<8>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        constexpr int m = (i & 3) | ((i >> 2) << 3);  // slot bit 2 clear
+        swap_l4(v[m], v[m | 4]);
+    });
+    static_for<8>([&](auto ic) {
+        constexpr int m = decltype(ic)::value;  // slot bit 3 clear
+        swap_l5(v[m], v[m | 8]);
+    });
+}
+
+template <bool INV, bool DIF>
+__device__ __forceinline__ void shuffle4096_r16(float2 (&v)[16], const float2* w) {
+    if constexpr (!DIF) {
+        static_for<15>([&](auto rc) {
+            constexpr int r = decltype(rc)::value + 1;
+            v[r] = tw_mul<INV>(v[r], w[r - 1]);
+        });
+    }
+    Dft<16, INV, float2>::run(v);
+    if constexpr (DIF) {
+        static_for<15>([&](auto rc) {
+            constexpr int r = decltype(rc)::value + 1;
+            v[r] = tw_mul<INV>(v[r], w[r - 1]);
+        });
+    }
+}
+
+// Transform (INV1, DIF), epi(0, m, z) on slot m = element shuffle4096_klow(tid)
+// + 256 m, transform (INV2, DIT); v in state A (element tid + 256 m) in and
+// out. lds: 2 x 4096 complex64 (one buffer per X1 direction).
+template <bool INV1, bool INV2, class Epi>
+__device__ __forceinline__ void shuffle4096_pair(float2 (&v)[16], int tid, const ShuffleTw4096& tw, float2* lds,
+                                                 Epi&& epi) {
+    shuffle4096_r16<INV1, true>(v, tw.p1);
+    shuffle4096_x1<true>(v, tid, lds);
+    shuffle4096_r16<INV1, true>(v, tw.p2);
+    shuffle4096_x2(v, tid);
+    Dft<16, INV1, float2>::run(v);
+    static_for<16>([&](auto mc) {
+        constexpr int m = decltype(mc)::value;
+        epi(0, m, v[m]);
+    });
+    Dft<16, INV2, float2>::run(v);
+    shuffle4096_x2(v, tid);
+    shuffle4096_r16<INV2, false>(v, tw.p2);
+    shuffle4096_x1<false>(v, tid, lds + kShuf4N);
+    shuffle4096_r16<INV2, false>(v, tw.p1);
+}
+
 }  // namespace slm

@@ -733,6 +733,11 @@ constexpr bool kLdsDouble = SLM_LDS_DOUBLE && K == 11;
 #ifndef SLM_SHUFFLE
 #define SLM_SHUFFLE 1
 #endif
+#ifndef SLM_SHUFFLE4096
+#define SLM_SHUFFLE4096 0  // A/B knob: the wave-shuffle pair for 4096-point GS rows
+#endif
+template <int K, int P>
+constexpr bool kShuffle4096 = SLM_SHUFFLE4096 && P == PREC_F32 && PlanOf<K>::N == kShuf4N && PlanOf<K>::E == 16;
 template <int K, int P>
 constexpr bool kShuffle = SLM_SHUFFLE && P == PREC_F32 && PlanOf<K>::N == kShufN && PlanOf<K>::E == 8;
 
@@ -763,7 +768,11 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
     using X = XchgOf<P, (long long)RPW * LINE, K>;
     using V = StateOf<P, X>;
     constexpr int ALT = kLdsDouble<K, false> ? RPW * LINE : 0;
-    __shared__ X smem[(ALT ? 2 : 1) * RPW * LINE];
+    // wave-shuffle pair for 4096-point rows (fft_shuffle.hpp; float32 GS, one row per workgroup)
+    constexpr bool SHUF4 = kShuffle4096<K, P> && MODE == ROW_GS_MAIN && RPW == 1 && L == 1 &&
+                           RowCfg<K>::THREADS == 256 && std::is_same_v<X, float2>;
+    constexpr int SMEM_ROW = (ALT ? 2 : 1) * RPW * LINE;
+    __shared__ X smem[SHUF4 && SMEM_ROW < 2 * kShuf4N ? 2 * kShuf4N : SMEM_ROW];
 
     // lane -> (row group within the quad, transform thread t): TL consecutive
     // t of one row group, then the next group of the quad. One wave instruction
@@ -798,8 +807,11 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
     static_assert(!SHUF || (std::is_same_v<X, float2> && sizeof(smem) >= 4 * kShufN * sizeof(float2)),
                   "the shuffle pair needs two 2-line complex64 exchange buffers");
     ShuffleTw stw;
+    ShuffleTw4096 stw4;
     if constexpr (SHUF)
         load_shuffle_tw(stw, threadIdx.x, static_cast<const float2*>(p.tw) + twiddle_count_key(K));
+    else if constexpr (SHUF4)
+        load_shuffle4096_tw(stw4, threadIdx.x, static_cast<const float2*>(p.tw) + twiddle_count_key(K));
     else
         load_twiddles<K, C>(tw, t, p.tw);
 
@@ -871,7 +883,15 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
         } else if constexpr (MODE == ROW_GS_MAIN) {
             // A -> B = a_in A/|A| (src/algorithms.py:30)
             auto epi = [&](int l, int m, C& z) { z = unit_scale(z, ain_at(l, m)); };
-            if constexpr (SHUF)
+            if constexpr (SHUF4) {
+                // the pair's middle holds element shuffle4096_klow(tid) + 256 m
+                const int km = shuffle4096_klow(threadIdx.x);
+                shuffle4096_pair<true, false>(v[0], threadIdx.x, stw4, reinterpret_cast<float2*>(smem),
+                                              [&](int, int m, C& z) {
+                                                  const S a = p.ain ? (S)p.ain[roff + km + T * m] : (S)1;
+                                                  z = unit_scale(z, a);
+                                              });
+            } else if constexpr (SHUF)
                 shuffle_pair<true, false>(v[0], threadIdx.x, stw, reinterpret_cast<float2*>(smem), epi);
             else
                 fft_pair<K, true, false, C>(v, t, tw, lds, epi);

@@ -126,8 +126,8 @@ int get_twiddles(int pk, int prec, const void** out) {
         host.push_back(1.0);
         host.push_back(0.0);
     }
-    if (pl.n == kShufN && pl.e == 8) {
-        // the wave-shuffle pair's table (fft_shuffle.hpp): the N roots
+    if ((pl.n == kShufN && pl.e == 8) || (pl.n == kShuf4N && pl.e == 16)) {
+        // the wave-shuffle pairs' table (fft_shuffle.hpp): the N roots
         // exp(-2 pi i e / N), after the Stockham entries (twiddle_count_key)
         for (int e = 0; e < pl.n; ++e) {
             const double ang = -2.0 * M_PI * (double)e / (double)pl.n;
