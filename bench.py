@@ -132,6 +132,40 @@ def pmc_traffic(config_key: str):
         return None
 
 
+def rocprof_kernels(config_key: str):
+    """The committed rocprofv3 kernel-trace summary of this configuration
+    (profiles/rocprof_kernels.json, written by tools/frac_check.py from a
+    `rocprofv3 --kernel-trace --stats` run of this bench): per kernel class
+    the trace's average duration over every launch, over the launches of the
+    event-timed run, and the event timing bench.py printed in that same run."""
+    path = os.path.join(ROOT, "profiles", "rocprof_kernels.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get(config_key)
+    except (OSError, ValueError):
+        return None
+
+
+def rank_diagnostics(plan, counts, rank, local_elapsed, steps, rows):
+    """What one rank did in the timed region, for the scaling run to break
+    down (rank 0 prints every rank's record): its device, its own wall time,
+    its kernels' HIP-event times, and the phase gather timed on its own with
+    events (collective: every rank calls this)."""
+    gather_ms, gather_bytes = plan.time_gather(counts, root=0, reps=5)
+    dev = plan.device
+    try:
+        bus = _lib.pci_bus_id(dev)
+    except _lib.SlmError:
+        bus = None
+    kern = {k: round(v["avg_us"], 3) for k, v in rows.items()}
+    run_us = sum(v["total_us"] for v in rows.values())
+    return {"rank": rank, "device": dev, "pci_bus_id": bus, "holograms": int(counts[rank]),
+            "step_ms": round(local_elapsed / steps * 1e3, 4), "kernel_avg_us": kern,
+            "iteration_kernels_ms_per_run": round(run_us / 1e3, 4),
+            "gather_ms": round(gather_ms, 4), "gather_bytes_to_root": gather_bytes,
+            "gather_gbs": round(gather_bytes / (gather_ms * 1e-3) / 1e9, 2) if gather_bytes and gather_ms > 0 else None}
+
+
 def cpu_baseline(n: int, iters: int, budget_s: float):
     """The repo's NumPy restatement of the reference (faithful float64, scipy.fft
     single thread, 1 core, as the reference runs) on the same synthetic target,
@@ -267,6 +301,7 @@ def main():
     for _ in range(opt.steps):
         step()
     plan.sync()
+    local_elapsed = time.perf_counter() - t0
     group.barrier()
     elapsed = group.max(time.perf_counter() - t0)
 
@@ -276,6 +311,7 @@ def main():
 
     dom, rows, _, _ = kernel_roofline(plan, iters)
     info = plan.info()
+    ranks = group.gather(rank_diagnostics(plan, counts, rank, local_elapsed, opt.steps, rows))
     # sanity on rank 0 over EVERY hologram of the job: the gathered phases are
     # finite and each gathered error curve (slm_plan_gather_stats, the
     # error_evolution of src/generate_hologram_sequence.py:19-31) decreases
@@ -302,6 +338,7 @@ def main():
     iter_s = ms_per_step / iters / 1e3
     roofline = {"bound": "hbm", "achieved": round(dr["achieved_gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(dr["achieved_gbs"] / HBM_PEAK_GBS, 4),
+                "frac_physical": round(dr["physical_gbs"] / HBM_PEAK_GBS, 4),
                 "traffic": None if traffic is None else traffic.get(dom),
                 "kernel": dom, "avg_us": round(dr["avg_us"], 3),
                 "bytes_model": "SURVEY.md 8d: GS 68 B/px/iteration = col_main 36 (two column passes 16+16, "
@@ -326,6 +363,18 @@ def main():
     copy["dominant_frac_of_copy_hbm"] = round(dr["achieved_gbs"] / copy["hbm_1gib_gbs"], 4)
     copy["dominant_physical_frac_of_copy_working_set"] = round(dr["physical_gbs"] / copy["working_set_gbs"], 4)
     roofline["measured_copy"] = copy
+    prof = rocprof_kernels(key)
+    if prof and dom in prof.get("kernels", {}):
+        pk = prof["kernels"][dom]
+        # the same frac from the committed rocprofv3 trace of this bench (the trace's
+        # mean over every launch, and over the launches bench.py timed with events in
+        # that run, beside those events: the offset the tracer adds per launch)
+        roofline["rocprof"] = {"source": prof.get("source"), "avg_us_all": pk.get("avg_us_all"),
+                               "avg_us_timed_run": pk.get("avg_us_timed_run"),
+                               "event_avg_us_same_run": pk.get("event_avg_us_same_run"),
+                               "frac_from_profile": round(dr["model_bytes_per_launch"] / (pk["avg_us_timed_run"] * 1e-6)
+                                                          / 1e9 / HBM_PEAK_GBS, 4)
+                               if pk.get("avg_us_timed_run") else None}
     out = {
         "metric": METRIC, "value": round(value, 3), "unit": "holograms/s", "n_gpus": world,
         "steps": opt.steps, "warmup": opt.warmup, "ms_per_step": round(ms_per_step, 4),
@@ -339,6 +388,7 @@ def main():
         "gs_iter_ms": round(ms_per_step / iters, 5),
         "roofline": roofline,
         "check": "ok" if ok else "FAILED",
+        "ranks": ranks,
     }
     if world == 1 and not opt.no_extra:
         extra = {"pcie_inclusive": pcie_inclusive(plan, targets(0, bper, n), iters)}

@@ -63,6 +63,8 @@ int slm_device_count(void);
 const char* slm_last_error(void);
 const char* slm_version(void);
 int slm_supported_length(int n);    /* 1 if n is a supported row/column length */
+/* PCI bus id ("0000:05:00.0") of a HIP device: which GPU a rank ran on */
+int slm_device_pci_bus_id(int device, char* buf, int len);
 /* Measured streaming-copy rate (read + write bytes / s, in GB/s) of two
  * `bytes`-sized device buffers on the current device, `reps` timed copies
  * (16 B per lane, grid-stride): the practical peak next to the 8 TB/s spec
@@ -135,6 +137,8 @@ int slm_plan_layout(slm_plan* plan, int* x_log2, int* y_log2);
  * point lines, float32; v_permlane swaps for four of the six exchanges; the
  * GS and GD iteration kernels) */
 int slm_plan_engine(slm_plan* plan, int* col_engine, int* row_engine);
+/* HIP device the plan lives on */
+int slm_plan_device(slm_plan* plan);
 
 /* Diagnostics: per-workgroup phase timestamps (s_memrealtime, 100 MHz: tile
  * start, loads complete, transforms done, stores complete, kernel entry) plus
@@ -162,6 +166,11 @@ int slm_gd(const void* tgt, int tgt_type, const float* ain, int batch, int heigh
 int slm_gs_multi(int n_gpus, const int* devices, const void* tgt, int tgt_type, const float* ain, int batch,
                  int height, int width, int max_loops, double tol, const float* init_phase, float* out_phase,
                  float* out_expected, double* out_stats, int* out_iters);
+/* Per-shard timing of the calling process's last slm_gs_multi: wall_ms[r] =
+ * shard r's whole thread (plan, upload, run, read back), run_ms[r] = its run
+ * alone (enqueue to stream drained); up to max_shards values each (either
+ * pointer may be NULL). Returns the number of shards of that call (0 if none). */
+int slm_gs_multi_timing(int max_shards, double* wall_ms, double* run_ms);
 
 /* unscaled 2-D C2C transform of [batch][h][w] complex64 (test entry) */
 int slm_fft2(const float* in_re_im, float* out_re_im, int batch, int height, int width, int inverse);
@@ -184,6 +193,12 @@ int slm_plan_gather_phase(slm_plan* plan, const int* counts, int root, float* ho
  * sum(counts) ints (iterations executed, -1 = all), rank order; either may be
  * NULL. */
 int slm_plan_gather_stats(slm_plan* plan, const int* counts, int root, double* stats_out, int* iters_out);
+/* Diagnostics of the phase gather (collective, every rank calls it): drains
+ * the plan stream, then times `reps` device-side slm_plan_gather_phase calls
+ * with HIP events on the plan stream; *ms = average per gather on this rank,
+ * *bytes_out = bytes this rank sends to root per gather (0 on root, whose own
+ * slab is a device-local copy). */
+int slm_plan_time_gather(slm_plan* plan, const int* counts, int root, int reps, double* ms, long long* bytes_out);
 /* Element offsets of a rank-order gather: offsets[r] = per_item x sum(counts[:r]),
  * offsets[nranks] = the total (offsets holds nranks + 1 values). The arithmetic
  * every gather above uses; host-only, needs no device. */

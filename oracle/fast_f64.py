@@ -62,14 +62,17 @@ def _unit_into(out, z, a, s):
 
 
 def gerchberg_saxton_f64(demanded_output, loops, initial_phase=None, incoming_intensity=None, tolerance=0.0,
-                         workers=None):
+                         workers=None, snapshots=None):
     """src/algorithms.py:10-49 in complex128 with z/|z| projections.
 
     ``initial_phase`` continues a run whose returned hologram was
     ``initial_phase`` (the GS loop state is angle(A) only). The incoming
     amplitude is float64 here (a uint8 intensity image makes the reference's
     amplitude float16 and its loop complex64: the faithful restatement). Returns
-    (angle(A) float64, expected_outcome float64, error_evolution list)."""
+    (angle(A) float64, expected_outcome float64, error_evolution list).
+    ``snapshots``: a dict whose keys are iteration counts < ``loops``; each is
+    filled with angle(A) after that many iterations (what a run of that length
+    would return), so one oracle run serves several gates."""
     pool = _Pool(workers or DEFAULT_WORKERS)
     try:
         t = np.asarray(demanded_output)
@@ -111,6 +114,8 @@ def gerchberg_saxton_f64(demanded_output, loops, initial_phase=None, incoming_in
             error = sum(pool.run(err_part, h)) / (h * w)
             err_evol.append(np.float64(error))
             i += 1
+            if snapshots is not None and i in snapshots and i < loops:
+                snapshots[i] = np.angle(a)
         return np.angle(a), expected, err_evol
     finally:
         pool.close()

@@ -53,6 +53,7 @@ _SIGNATURES = [
     ("slm_last_error", ctypes.c_char_p, []),
     ("slm_version", ctypes.c_char_p, []),
     ("slm_supported_length", _c_int, [_c_int]),
+    ("slm_device_pci_bus_id", _c_int, [_c_int, ctypes.c_char_p, _c_int]),
     ("slm_copy_bandwidth", _c_int, [ctypes.c_longlong, _c_int, _P(_c_double)]),
     ("slm_plan_create", _c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _P(_vp)]),
     ("slm_plan_destroy", _c_int, [_vp]),
@@ -75,6 +76,7 @@ _SIGNATURES = [
     ("slm_plan_info", _c_int, [_vp, _vp]),
     ("slm_plan_layout", _c_int, [_vp, _vp, _vp]),
     ("slm_plan_engine", _c_int, [_vp, _vp, _vp]),
+    ("slm_plan_device", _c_int, [_vp]),
     ("slm_plan_read_trace", _c_int, [_vp, _c_int, _vp]),
     ("slm_gs", _c_int, [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_double, _vp, _vp, _vp, _vp, _vp]),
     ("slm_gd", _c_int,
@@ -82,11 +84,13 @@ _SIGNATURES = [
     ("slm_fft2", _c_int, [_vp, _vp, _c_int, _c_int, _c_int, _c_int]),
     ("slm_gs_multi", _c_int, [_c_int, _vp, _vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_double, _vp, _vp,
                               _vp, _vp, _vp]),
+    ("slm_gs_multi_timing", _c_int, [_c_int, _vp, _vp]),
     ("slm_comm_unique_id", _c_int, [_vp]),
     ("slm_comm_init", _c_int, [_c_int, _c_int, _vp]),
     ("slm_comm_destroy", _c_int, []),
     ("slm_plan_gather_phase", _c_int, [_vp, _vp, _c_int, _vp]),
     ("slm_plan_gather_stats", _c_int, [_vp, _vp, _c_int, _vp, _vp]),
+    ("slm_plan_time_gather", _c_int, [_vp, _vp, _c_int, _c_int, _P(_c_double), _P(ctypes.c_longlong)]),
     ("slm_gather_layout", _c_int, [_c_int, _vp, ctypes.c_longlong, _vp]),
     ("slm_trap_frames", _c_int,
      [_c_int, _c_int, _c_int, _vp, _vp, _vp, _c_double, _c_int, _vp, _vp]),
@@ -158,6 +162,21 @@ def init(device: int | None = None) -> None:
 
 def device_count() -> int:
     return int(load().slm_device_count())
+
+
+def pci_bus_id(device: int) -> str:
+    """PCI bus id of a HIP device (slm_device_pci_bus_id)."""
+    buf = ctypes.create_string_buffer(64)
+    check(load().slm_device_pci_bus_id(int(device), buf, 64), "slm_device_pci_bus_id")
+    return buf.value.decode()
+
+
+def gs_multi_timing(max_shards: int = 64):
+    """(wall_ms, run_ms) per shard of this process's last gs_multi call."""
+    wall = np.zeros(max_shards, np.float64)
+    run = np.zeros(max_shards, np.float64)
+    n = int(load().slm_gs_multi_timing(int(max_shards), ptr(wall), ptr(run)))
+    return wall[:min(n, max_shards)].tolist(), run[:min(n, max_shards)].tolist()
 
 
 def copy_bandwidth(nbytes: int, reps: int = 20) -> float:
@@ -293,6 +312,21 @@ class Plan:
                 "row_threads": int(a[3]), "rows_per_workgroup": int(a[4]), "row_plan": int(a[5]),
                 "col_plan": int(a[6]), "precision": "f64" if a[7] == PRECISION_F64 else "f32",
                 "layout": self.layout(), "engine": self.engine()}
+
+    @property
+    def device(self) -> int:
+        """HIP device of the plan (slm_plan_device)."""
+        return int(self._lib.slm_plan_device(self.handle))
+
+    def time_gather(self, counts, root: int = 0, reps: int = 5):
+        """(ms per device-side phase gather, bytes this rank sends per gather):
+        slm_plan_time_gather, collective."""
+        c = np.ascontiguousarray(counts, dtype=np.int32)
+        ms = ctypes.c_double()
+        nb = ctypes.c_longlong()
+        check(self._lib.slm_plan_time_gather(self.handle, ptr(c), int(root), int(reps), ctypes.byref(ms),
+                                             ctypes.byref(nb)), "slm_plan_time_gather")
+        return float(ms.value), int(nb.value)
 
     def engine(self) -> tuple[str, str]:
         """(column, row) transform engine of the GS iteration kernels:

@@ -55,12 +55,17 @@ def target_for_device(demanded_output) -> tuple[np.ndarray, int]:
     return np.ascontiguousarray(t, dtype=np.float32), TGT_F32
 
 
+def _needs_exact_stats(t) -> bool:
+    """True for target dtypes that float32 does not hold exactly (float64, wide integers)."""
+    return not (t.dtype in (np.uint8, np.float32, np.float16) or (t.dtype.kind in "iu" and t.dtype.itemsize <= 2))
+
+
 def _exact_target_stats(plan, t):
     """A target that float32 does not hold exactly (float64, wide integers)
     keeps norm = np.amax(T) (src/algorithms.py:23) and sum T^2 (error_f's
     constant term, :161-162) in float64; the cross term sum E*T uses the
     float32 device copy (relative effect <= 2^-24 per pixel)."""
-    if t.dtype in (np.uint8, np.float32, np.float16) or (t.dtype.kind in "iu" and t.dtype.itemsize <= 2):
+    if not _needs_exact_stats(t):
         return
     tf = t.astype(np.float64).reshape(plan.batch, -1)
     plan.set_target_stats(tf.max(axis=1), np.einsum("ij,ij->i", tf, tf))
@@ -182,8 +187,14 @@ def run_gs(targets, loops, tol=0.0, ain=None, initial_phase=None):
 
 def run_gs_multi(targets, loops, devices, tol=0.0, ain=None):
     """run_gs's contract over several GPUs from this one process
-    (slm_gs_multi: contiguous shards, one host thread / plan per device)."""
+    (slm_gs_multi: contiguous shards, one host thread / plan per device).
+    slm_gs_multi takes the error's constant terms from its float32 copy of the
+    target, so frames that float32 does not hold exactly (float64, wide
+    integers) go through run_gs, which keeps them in float64 (the two paths
+    then report the same error_evolution)."""
     t = np.asarray(targets)
+    if _needs_exact_stats(t):
+        return run_gs(t, loops, tol, ain)
     tdev, _ = target_for_device(t)
     phase, e, stats, iters = _lib.gs_multi(tdev, loops, devices, tol=tol, ain=ain)
     norm = t.reshape(t.shape[0], -1).max(axis=1).astype(np.float64)  # np.amax(demanded_output)

@@ -7,6 +7,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <climits>
 #include <cmath>
 #include <cstdarg>
@@ -305,6 +306,7 @@ struct slm_plan {
     int skip_wg_plus1 = 0;  // $SLM_GD_FAULT_TEST: fused-path fault injection (tests)
     int gd_recoveries = 0;  // runs redone on the two-launch path after a grid fault
     float2* field0 = nullptr;  // GD: host-set initial field (blocked), never overwritten by a run
+    bool field_fresh = false;  // set_field since the last run: the plan's field is field0
     // parameters of the last enqueued run (a grid fault reruns it)
     int last_loops = 0, last_checked = 0;
     double last_tol = 0.0;
@@ -772,6 +774,7 @@ int enqueue_run(slm_plan* p, int loops, double tol, int checked, float wa) {
         return fail(SLM_ERR_ARG, "loops %d outside [1, %d]", loops, p->max_loops);
     if (p->algo == SLM_ALGO_GD && !p->lr_set) return fail(SLM_ERR_STATE, "learning rates not set");
     HIP_TRY(hipSetDevice(p->device));
+    p->field_fresh = false;  // the run writes the field
     RC(launch(p, SLM_KERNEL_OTHER, fill_int_kernel, dim3((p->B + 255) / 256), dim3(256), p->stop, p->B,
               (int)INT_MAX));
     RC(p->algo == SLM_ALGO_GS ? enqueue_gs(p, loops, tol, checked) : enqueue_gd(p, loops, tol, checked, wa));
@@ -852,11 +855,14 @@ int slm_copy_bandwidth(long long bytes, int reps, double* gbs) {
         // enough workgroups that a working-set-sized copy still fills the chip
         const int grid = (int)std::max<long long>(1, std::min<long long>((long long)cus * 32, (n + 1023) / 1024));
         hipLaunchKernelGGL(copy_f4_kernel, dim3(grid), dim3(256), 0, st, a, b, n);  // warm-up
-        hip(hipEventRecord(e0, st));
-        for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(copy_f4_kernel, dim3(grid), dim3(256), 0, st, a, b, n);
-        float ms = 0.f;
-        if (hip(hipEventRecord(e1, st)) && hip(hipEventSynchronize(e1)) && hip(hipEventElapsedTime(&ms, e0, e1)))
-            *gbs = 2.0 * 16.0 * (double)n * reps / (ms * 1e-3) / 1e9;
+        // a failed launch would leave the event pair timing an empty stream
+        if (hip(hipGetLastError()) && hip(hipEventRecord(e0, st))) {
+            for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(copy_f4_kernel, dim3(grid), dim3(256), 0, st, a, b, n);
+            float ms = 0.f;
+            if (hip(hipGetLastError()) && hip(hipEventRecord(e1, st)) && hip(hipEventSynchronize(e1)) &&
+                hip(hipEventElapsedTime(&ms, e0, e1)))
+                *gbs = 2.0 * 16.0 * (double)n * reps / (ms * 1e-3) / 1e9;
+        }
     }
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
@@ -869,6 +875,12 @@ int slm_copy_bandwidth(long long bytes, int reps, double* gbs) {
 const char* slm_version(void) { return "libslm_hip 0.1 (gfx950)"; }
 
 int slm_supported_length(int n) { return plan_index(n) >= 0 ? 1 : 0; }
+
+int slm_device_pci_bus_id(int device, char* buf, int len) {
+    if (!buf || len < 13) return fail(SLM_ERR_ARG, "need a buffer of at least 13 bytes");
+    HIP_TRY(hipDeviceGetPCIBusId(buf, len, device));
+    return 0;
+}
 
 }  // extern "C"
 
@@ -1091,6 +1103,7 @@ int slm_plan_set_field(slm_plan* p, const float* field) {
     RC(relayout(layout_y_log2(p->lid), (const float2*)p->y, p->field0, n, p->H, p->W, true, p->stream));
     HIP_TRY(hipStreamSynchronize(p->stream));
     p->field_set = true;
+    p->field_fresh = true;
     return 0;
 }
 
@@ -1107,6 +1120,7 @@ int slm_plan_set_lr(slm_plan* p, const float* lr) {
 int slm_plan_run(slm_plan* p, int loops, double tol, int checked, float wa) {
     if (p) {
         p->timing = false;
+        p->field_fresh = false;  // replays skip enqueue_run
         p->last_loops = loops;
         p->last_tol = tol;
         p->last_checked = checked;
@@ -1267,6 +1281,8 @@ int slm_plan_engine(slm_plan* p, int* col_engine, int* row_engine) {
     return 0;
 }
 
+int slm_plan_device(slm_plan* p) { return p ? p->device : -1; }
+
 int slm_plan_layout(slm_plan* p, int* x_log2, int* y_log2) {
     if (!p || !x_log2 || !y_log2) return fail(SLM_ERR_ARG, "null argument");
     *x_log2 = layout_x_log2(p->lid);
@@ -1303,6 +1319,22 @@ int slm_gd(const void* tgt, int tgt_type, const float* ain, int batch, int heigh
     return rc;
 }
 
+namespace {
+// per-shard timing of the last slm_gs_multi of this process (slm_gs_multi_timing)
+std::mutex g_multi_mu;
+std::vector<double> g_multi_wall, g_multi_run;
+}  // namespace
+
+int slm_gs_multi_timing(int max_shards, double* wall_ms, double* run_ms) {
+    std::lock_guard<std::mutex> lk(g_multi_mu);
+    const int n = (int)g_multi_wall.size();
+    for (int r = 0; r < n && r < max_shards; ++r) {
+        if (wall_ms) wall_ms[r] = g_multi_wall[r];
+        if (run_ms) run_ms[r] = g_multi_run[r];
+    }
+    return n;
+}
+
 int slm_gs_multi(int n_gpus, const int* devices, const void* tgt, int tgt_type, const float* ain, int batch,
                  int height, int width, int max_loops, double tol, const float* init_phase, float* out_phase,
                  float* out_expected, double* out_stats, int* out_iters) {
@@ -1326,8 +1358,12 @@ int slm_gs_multi(int n_gpus, const int* devices, const void* tgt, int tgt_type, 
     const size_t tb = tgt_type == SLM_TGT_U8 ? 1 : 4;
     std::vector<int> rcs(n_gpus, 0);
     std::vector<std::string> errs(n_gpus);
+    std::vector<double> wall(n_gpus, 0.0), run(n_gpus, 0.0);
+    using clk = std::chrono::steady_clock;
+    auto ms_since = [](clk::time_point t0) { return std::chrono::duration<double, std::milli>(clk::now() - t0).count(); };
     auto shard = [&](int r) {
         if (!counts[r]) return;
+        const auto t0 = clk::now();
         const long long h0 = off[r];
         slm_plan* p = nullptr;
         int rc = plan_create_on(dev[r], SLM_ALGO_GS, counts[r], height, width, tgt_type, ain != nullptr, max_loops,
@@ -1335,7 +1371,10 @@ int slm_gs_multi(int n_gpus, const int* devices, const void* tgt, int tgt_type, 
         if (!rc) rc = slm_plan_set_target(p, static_cast<const char*>(tgt) + (size_t)h0 * holo * tb);
         if (!rc && ain) rc = slm_plan_set_ain(p, ain);
         if (!rc && init_phase) rc = slm_plan_set_phase(p, init_phase + h0 * holo);
+        const auto t1 = clk::now();
         if (!rc) rc = slm_plan_run(p, max_loops, tol, tol > 0.0 ? 1 : 0, 0.f);
+        if (!rc) rc = slm_plan_sync(p);
+        run[r] = ms_since(t1);
         // each shard lands in its own slice of the caller's arrays over its GPU's own link
         if (!rc)
             rc = slm_plan_read(p, out_phase ? out_phase + h0 * holo : nullptr,
@@ -1345,6 +1384,7 @@ int slm_gs_multi(int n_gpus, const int* devices, const void* tgt, int tgt_type, 
         if (rc) errs[r] = g_err;  // thread-local message of this shard's thread
         free_plan(p);
         rcs[r] = rc;
+        wall[r] = ms_since(t0);
     };
     if (n_gpus == 1) {
         shard(0);
@@ -1352,6 +1392,11 @@ int slm_gs_multi(int n_gpus, const int* devices, const void* tgt, int tgt_type, 
         std::vector<std::thread> th;
         for (int r = 0; r < n_gpus; ++r) th.emplace_back(shard, r);
         for (auto& t : th) t.join();
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_multi_mu);
+        g_multi_wall = wall;
+        g_multi_run = run;
     }
     for (int r = 0; r < n_gpus; ++r)
         if (rcs[r]) return fail(rcs[r], "shard %d (device %d): %s", r, dev[r], errs[r].c_str());
@@ -1419,8 +1464,10 @@ int slm_plan_read_field(slm_plan* p, float* field) {
     if (p->algo != SLM_ALGO_GD) return fail(SLM_ERR_STATE, "the field is the state of GD plans");
     HIP_TRY(hipSetDevice(p->device));
     const long long n = (long long)p->B * p->holo;
-    // p->y is scratch between runs (every run rewrites it before reading it)
-    RC(relayout(layout_y_log2(p->lid), (const float2*)p->field, p->y, n, p->H, p->W, false, p->stream));
+    // p->y is scratch between runs (every run rewrites it before reading it); a
+    // field set since the last run is read back from field0 (runs never write it)
+    const float2* src = p->field_fresh ? p->field0 : p->field;
+    RC(relayout(layout_y_log2(p->lid), src, p->y, n, p->H, p->W, false, p->stream));
     HIP_TRY(hipStreamSynchronize(p->stream));
     RC(copy_sync(field, p->y, (size_t)n * sizeof(float2), hipMemcpyDeviceToHost, p->stream));
     return 0;
@@ -1488,6 +1535,9 @@ int gather_slab(slm_plan* p, const void* src, long long per_item, size_t elem, n
     const int me = g_comm ? g_comm_rank : 0;
     if (root < 0 || root >= n) return fail(SLM_ERR_ARG, "root %d outside [0, %d)", root, n);
     if (counts[me] != p->B) return fail(SLM_ERR_ARG, "counts[%d]=%d but the plan holds %d", me, counts[me], p->B);
+    // a GD run on the one-launch column side may have faulted (its grid wait gave
+    // up): settle it -- redo it on two launches -- before its results leave this rank
+    if (p->gfault) RC(slm_plan_sync(p));
     std::vector<long long> off(n + 1);
     RC(slm_gather_layout(n, counts, per_item, off.data()));
     if (me == root) {
@@ -1532,6 +1582,28 @@ int slm_plan_gather_phase(slm_plan* p, const int* counts, int root, float* host_
     if (!p) return fail(SLM_ERR_ARG, "null plan");
     return gather_slab(p, p->phase_out, p->holo, sizeof(float), ncclFloat32, counts, root, (void**)&p->gather_buf,
                        &p->gather_elems, host_out);
+}
+
+int slm_plan_time_gather(slm_plan* p, const int* counts, int root, int reps, double* ms, long long* bytes_out) {
+    if (!p || !counts || !ms || reps < 1) return fail(SLM_ERR_ARG, "bad gather-timing arguments");
+    RC(slm_plan_sync(p));
+    const int me = g_comm ? g_comm_rank : 0;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    int rc = 0;
+    float t = 0.f;
+    if (hipEventRecord(e0, p->stream) != hipSuccess) rc = fail(SLM_ERR_HIP, "event record failed");
+    for (int i = 0; i < reps && !rc; ++i) rc = slm_plan_gather_phase(p, counts, root, nullptr);
+    if (!rc && (hipEventRecord(e1, p->stream) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+                hipEventElapsedTime(&t, e0, e1) != hipSuccess))
+        rc = fail(SLM_ERR_HIP, "gather timing events failed");
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (rc) return rc;
+    *ms = (double)t / reps;
+    if (bytes_out) *bytes_out = me == root ? 0 : (long long)p->B * p->holo * (long long)sizeof(float);
+    return 0;
 }
 
 int slm_plan_gather_stats(slm_plan* p, const int* counts, int root, double* stats_out, int* iters_out) {

@@ -19,8 +19,11 @@ from __future__ import annotations
 import hmac
 import os
 import pickle
+import secrets
 import socket
+import stat
 import struct
+import tempfile
 import time
 
 
@@ -72,9 +75,55 @@ _MAX_TOKEN = 256
 
 
 def job_token() -> bytes:
-    """Shared secret of one job's ranks: $SLM_JOB_TOKEN (bench.py's own
-    launcher draws a random one), else torchrun's per-job run id."""
-    return (os.environ.get("SLM_JOB_TOKEN") or os.environ.get("TORCHELASTIC_RUN_ID") or "").encode()[:_MAX_TOKEN]
+    """Shared secret of one job's ranks from the launcher: $SLM_JOB_TOKEN
+    (bench.py's own launcher draws a random one), else torchrun's per-job run
+    id -- unless that is empty or the constant 'none' a non-standalone torchrun
+    sets, which admits nothing (b"": see local_token_file)."""
+    tok = os.environ.get("SLM_JOB_TOKEN") or ""
+    if not tok:
+        run_id = os.environ.get("TORCHELASTIC_RUN_ID") or ""
+        tok = "" if run_id.lower() in ("", "none") else run_id
+    return tok.encode()[:_MAX_TOKEN]
+
+
+def _is_local(addr: str) -> bool:
+    return addr in ("127.0.0.1", "localhost", "::1") or addr.startswith("127.")
+
+
+def local_token_file(port: int) -> str:
+    """Where rank 0 of a single-host job whose launcher gave no secret leaves a
+    fresh random token for the other ranks: a file only this user can read, in
+    a directory only this user can enter (checked, never followed through a
+    link). Local ranks of the same job run as the same user; a process of
+    another user cannot read it, so it cannot pass the hello."""
+    d = os.path.join(tempfile.gettempdir(), f"slm-ctl-{os.getuid()}")
+    try:
+        os.mkdir(d, 0o700)
+    except FileExistsError:
+        pass
+    st = os.lstat(d)
+    if not stat.S_ISDIR(st.st_mode) or st.st_uid != os.getuid() or st.st_mode & 0o077:
+        raise PermissionError(f"{d} is not a private directory of this user; set SLM_JOB_TOKEN")
+    return os.path.join(d, f"job-{port}.token")
+
+
+def _write_token_file(path: str) -> bytes:
+    tok = secrets.token_hex(16).encode()
+    tmp = f"{path}.{os.getpid()}"
+    fd = os.open(tmp, os.O_WRONLY | os.O_CREAT | os.O_EXCL, 0o600)
+    with os.fdopen(fd, "wb") as f:
+        f.write(tok)
+    os.replace(tmp, path)
+    return tok
+
+
+def _read_token_file(path: str) -> bytes | None:
+    try:
+        fd = os.open(path, os.O_RDONLY | getattr(os, "O_NOFOLLOW", 0))
+    except FileNotFoundError:
+        return None
+    with os.fdopen(fd, "rb") as f:
+        return f.read(_MAX_TOKEN)
 
 
 def _send(sock, obj) -> None:
@@ -99,6 +148,9 @@ def _recv(sock):
     if n > MAX_MESSAGE:
         raise ConnectionError(f"control-plane message of {n} bytes exceeds {MAX_MESSAGE}")
     return pickle.loads(_recv_exact(sock, n))  # only peers that passed the hello check reach here
+
+
+_ACK = b"\x06"
 
 
 def _send_hello(sock, rank: int, token: bytes) -> None:
@@ -126,8 +178,12 @@ class Group:
 
     Every rank calls the same collectives in the same order. Rank 0 accepts
     WORLD_SIZE - 1 connections. A connection is admitted only after a raw-bytes
-    hello carrying the job token (job_token()); only then are messages --
-    length-prefixed pickles, at most MAX_MESSAGE bytes -- exchanged."""
+    hello carrying the job token (job_token(); when the launcher provides none
+    and the job is on this host, rank 0 draws one into local_token_file) and
+    acknowledged with one byte; only then are messages -- length-prefixed
+    pickles, at most MAX_MESSAGE bytes -- exchanged. A job spread over
+    several hosts must set $SLM_JOB_TOKEN (or run under a torchrun with a run
+    id)."""
 
     def __init__(self, rank: int, world_size: int, addr: str = "127.0.0.1", port: int | None = None,
                  timeout: float = 300.0):
@@ -152,6 +208,13 @@ class Group:
             srv.settimeout(timeout)
             peers: list[socket.socket | None] = [None] * world_size
             token = job_token()
+            token_path = None
+            if not token:
+                if not _is_local(addr):
+                    srv.close()
+                    raise RuntimeError("a multi-host control plane needs a job secret: set SLM_JOB_TOKEN")
+                token_path = local_token_file(port)
+                token = _write_token_file(token_path)
             deadline = time.monotonic() + timeout
             try:
                 while any(p is None for p in peers[1:]):
@@ -163,6 +226,7 @@ class Group:
                         r = _recv_hello(conn, world_size, token)
                         if peers[r] is not None:
                             raise ConnectionError(f"second control-plane hello from rank {r}")
+                        conn.sendall(_ACK)
                     except (ConnectionError, OSError):
                         conn.close()  # not one of this job's ranks: drop it, keep listening
                         continue
@@ -170,20 +234,40 @@ class Group:
                     peers[r] = conn
             finally:
                 srv.close()
+                if token_path is not None:
+                    try:
+                        os.unlink(token_path)  # every rank has joined (or the job failed)
+                    except OSError:
+                        pass
             self.peers = peers
         else:
             deadline = time.monotonic() + timeout
+            token = job_token()
+            token_path = None
+            if not token:
+                if not _is_local(addr):
+                    raise RuntimeError("a multi-host control plane needs a job secret: set SLM_JOB_TOKEN")
+                token_path = local_token_file(port)
             while True:
+                s = None
                 try:
+                    if token_path is not None:
+                        token = _read_token_file(token_path)  # rank 0's, once it has drawn it
+                        if token is None:
+                            raise ConnectionError("rank 0 has not published the job token yet")
                     s = socket.create_connection((addr, port), timeout=5.0)
+                    s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                    _send_hello(s, rank, token)
+                    if _recv_exact(s, 1) != _ACK:  # a refused hello (e.g. a stale token file) closes
+                        raise ConnectionError("control-plane hello not acknowledged")
                     break
                 except OSError:
+                    if s is not None:
+                        s.close()
                     if time.monotonic() > deadline:
                         raise
                     time.sleep(0.05)
             s.settimeout(timeout)
-            s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-            _send_hello(s, rank, job_token())
             self.sock = s
 
     @classmethod

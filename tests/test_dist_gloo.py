@@ -237,3 +237,51 @@ def test_control_plane_admits_only_this_jobs_ranks(monkeypatch):
         parallel._send(g1.sock, b"x" * (parallel.MAX_MESSAGE + 1))
     g0.close()
     g1.close()
+
+
+def test_control_plane_without_launcher_secret(monkeypatch):
+    """A launcher that gives no secret (no $SLM_JOB_TOKEN; a non-standalone
+    torchrun's TORCHELASTIC_RUN_ID is the constant 'none') still admits only
+    this job's ranks: rank 0 draws a token into a file only this user can read
+    (parallel.local_token_file), a stale file of an earlier job on the same
+    port is replaced, an empty or 'none' token is refused."""
+    import socket
+    import threading
+    import time
+
+    monkeypatch.delenv("SLM_JOB_TOKEN", raising=False)
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "none")
+    assert parallel.job_token() == b""
+    port = _free_port()
+    path = parallel.local_token_file(port)
+    with open(path, "wb") as f:
+        f.write(b"stale-token-of-an-earlier-job")
+    box = {}
+    th = threading.Thread(target=lambda: box.setdefault("g0", parallel.Group(0, 2, "127.0.0.1", port, timeout=30)))
+    th.start()
+    deadline = time.monotonic() + 10
+    while True:
+        try:
+            probe = socket.create_connection(("127.0.0.1", port), timeout=1)
+            break
+        except OSError:
+            assert time.monotonic() < deadline
+            time.sleep(0.02)
+    for bad in (b"", b"none", b"stale-token-of-an-earlier-job"):
+        parallel._send_hello(probe, 1, bad)
+        assert probe.recv(1) == b""  # dropped without an acknowledgement
+        probe.close()
+        probe = socket.create_connection(("127.0.0.1", port), timeout=5)
+    probe.close()
+    g1 = parallel.Group(1, 2, "127.0.0.1", port, timeout=30)
+    th.join(30)
+    g0 = box["g0"]
+    assert not os.path.exists(path)  # removed once every rank joined
+    assert os.stat(os.path.dirname(path)).st_mode & 0o077 == 0
+    out = {}
+    t2 = threading.Thread(target=lambda: out.setdefault(0, g0.all_gather(0)))
+    t2.start()
+    assert g1.all_gather(1) == [0, 1]
+    t2.join(10)
+    g0.close()
+    g1.close()

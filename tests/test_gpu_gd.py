@@ -81,3 +81,63 @@ def test_gd_other_guesses_vs_faithful_oracle(gpu, guess):
     # loop sits at 0.7e-6..1.0e-5 rms after 20 loops here, so the float32 floor
     # is the bound for these (the default "random" guess is gated at 1e-5).
     assert orc.phase_rms(holo, ph_o) < 3e-5
+
+
+@pytest.mark.gpu
+def test_read_field_after_set_field(gpu):
+    """slm_plan_read_field before any run returns the field just set (it lives
+    in the plan's initial-field buffer until a run writes the state), and
+    after a run the run's field."""
+    rng = np.random.default_rng(11)
+    t = rng.uniform(0, 255, (2, 128, 256)).astype(np.float32)
+    x0 = np.exp(1j * rng.uniform(-np.pi, np.pi, t.shape)).astype(np.complex64)
+    with gpu.Plan(gpu.ALGO_GD, 2, 128, 256, gpu.TGT_F32, False, 5) as p:
+        p.set_target(t)
+        p.set_field(x0)
+        np.testing.assert_array_equal(p.read_field(), x0)
+        p.set_lr(np.full(5, 0.005, np.float32))
+        p.run(5, white_attention=1.0)
+        x5 = p.read_field()
+        assert not np.array_equal(x5, x0)
+        p.set_field(x0 * 2)
+        np.testing.assert_array_equal(p.read_field(), x0 * 2)
+        p.run(5, white_attention=1.0)
+        assert not np.array_equal(p.read_field(), x0 * 2)
+
+
+@pytest.mark.gpu
+def test_gd_fault_settled_before_gather(gpu):
+    """A one-launch GD run whose grid wait gives up (SLM_GD_FAULT_TEST) is redone
+    on the two-launch path before slm_plan_gather_phase / _stats ship its
+    results (world size 1: the root's own slab), so the gathered phases and
+    statistics equal the two-launch run's."""
+    from spatial_light_modulator_module_amd import algorithms as alg
+
+    n, loops, b = 256, 12, 2
+    rng = np.random.default_rng(5)
+    t = rng.uniform(0, 255, (b, n, n)).astype(np.float32)
+    x0 = np.stack([alg.make_initial_guess("random", None, t[k], 42 + k) for k in range(b)])
+
+    def run(env):
+        old = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            with gpu.Plan(gpu.ALGO_GD, b, n, n, gpu.TGT_F32, False, loops) as p:
+                p.set_target(t)
+                p.set_field(x0)
+                p.set_lr(np.full(loops, 0.005, np.float32))
+                p.run(loops, white_attention=1.0)
+                ph = np.empty((b, n, n), np.float32)
+                p.gather_phase([b], root=0, host_out=ph)
+                st, it = p.gather_stats([b], root=0)
+                return ph, st, it, p.gd_recoveries
+        finally:
+            for k, v in old.items():
+                os.environ.pop(k, None) if v is None else os.environ.__setitem__(k, v)
+
+    ref = run({"SLM_GD_MODE": "two"})
+    got = run({"SLM_GD_FAULT_TEST": "3"})
+    assert got[3] == 1
+    np.testing.assert_array_equal(got[0], ref[0])
+    np.testing.assert_array_equal(got[1], ref[1])
+    np.testing.assert_array_equal(got[2], ref[2])

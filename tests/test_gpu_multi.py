@@ -127,3 +127,22 @@ def test_gs_multi_as_integration_binds_it(gpu):
     rph, _, rst, _ = _whole_batch(lib, t, 10)
     np.testing.assert_array_equal(ph, rph.astype(np.float64))
     assert errs == [list(s[:, 3]) for s in rst]
+
+
+@pytest.mark.gpu
+def test_run_gs_multi_exact_stats_frames(gpu):
+    """Frames that float32 does not hold exactly (float64 here) keep the
+    error's constant terms in float64: the sequence CLI's multi-GPU path
+    (algorithms.run_gs_multi) reports the same error_evolution as the
+    single-GPU path (algorithms.run_gs) for them, and for float32 frames."""
+    from spatial_light_modulator_module_amd import algorithms as alg
+
+    rng = np.random.default_rng(9)
+    t64 = rng.uniform(0, 255, (3, 128, 128))  # float64 frames
+    for t in (t64, t64.astype(np.float32)):
+        ph, e, errs, norm, emax = alg.run_gs_multi(t, 8, [0, 0])
+        rph, re, rerrs, rnorm, remax = alg.run_gs(t, 8)
+        np.testing.assert_array_equal(ph, rph)
+        np.testing.assert_array_equal(norm, rnorm)
+        for a, b in zip(errs, rerrs):
+            np.testing.assert_array_equal(a, b)
