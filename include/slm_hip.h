@@ -103,6 +103,12 @@ int slm_plan_run(slm_plan* plan, int loops, double tol, int checked, float white
 int slm_plan_run_timed(slm_plan* plan, int loops, double tol, int checked, float white_attention,
                        double* us_per_class, int* launches_per_class);
 int slm_plan_sync(slm_plan* plan);
+/* Device-side stopwatch on the plan stream: slm_plan_mark(plan, 0) and
+ * (plan, 1) record the plan's two HIP events; slm_plan_marked_ms waits for
+ * mark 1 and returns the device time between them (what bench.py's timed
+ * region took on the GPU, graph replays and gathers included). */
+int slm_plan_mark(slm_plan* plan, int which);
+int slm_plan_marked_ms(slm_plan* plan, double* ms);
 int slm_plan_gd_recoveries(slm_plan* plan); /* GD runs redone after a one-launch wait gave up */
 /* phase [batch][h][w] float32 (radians, angle convention of np.angle);
  * expected [batch][h][w] float32 = |C|^2 of the last iteration (scale by

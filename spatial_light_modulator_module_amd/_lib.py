@@ -67,6 +67,8 @@ _SIGNATURES = [
     ("slm_plan_run", _c_int, [_vp, _c_int, _c_double, _c_int, _c_float]),
     ("slm_plan_run_timed", _c_int, [_vp, _c_int, _c_double, _c_int, _c_float, _vp, _vp]),
     ("slm_plan_sync", _c_int, [_vp]),
+    ("slm_plan_mark", _c_int, [_vp, _c_int]),
+    ("slm_plan_marked_ms", _c_int, [_vp, _P(_c_double)]),
     ("slm_plan_gd_recoveries", _c_int, [_vp]),
     ("slm_plan_read", _c_int, [_vp, _vp, _vp, _vp, _vp]),
     ("slm_plan_read_target_stats", _c_int, [_vp, _vp, _vp]),
@@ -269,6 +271,16 @@ class Plan:
 
     def sync(self) -> None:
         check(self._lib.slm_plan_sync(self.handle), "slm_plan_sync")
+
+    def mark(self, which: int) -> None:
+        """Record stopwatch event 0 or 1 on the plan stream (slm_plan_mark)."""
+        check(self._lib.slm_plan_mark(self.handle, int(which)), "slm_plan_mark")
+
+    def marked_ms(self) -> float:
+        """Device time between marks 0 and 1 (slm_plan_marked_ms)."""
+        ms = ctypes.c_double()
+        check(self._lib.slm_plan_marked_ms(self.handle, ctypes.byref(ms)), "slm_plan_marked_ms")
+        return float(ms.value)
 
     @property
     def gd_recoveries(self) -> int:

@@ -358,7 +358,11 @@ struct TwCountOf<N, IntList<Rs...>> {
 //             785 -> 968 us: the table loads sit in the dependency chain), and
 //             the compiler contracts the products differently (not bitwise
 //             TW_CACHED). Kept for A/B builds (-DSLM_F32_ROW_TW=4).
-enum TwMode : int { TW_CACHED = 0, TW_DIRECT = 1, TW_POWERS = 2, TW_CHAIN = 3, TW_LAST = 4 };
+//  TW_SPLIT:  radix-16 passes only: per butterfly group w^1..w^3 and w^4,
+//             w^8, w^12 cached (exact table values), w^(4a+b) = w^(4a) w^b
+//             formed where used (one complex product, one rounding): 6
+//             registers-pairs per group instead of 15 (4096 16.16.16 plans).
+enum TwMode : int { TW_CACHED = 0, TW_DIRECT = 1, TW_POWERS = 2, TW_CHAIN = 3, TW_LAST = 4, TW_SPLIT = 5 };
 
 template <int N, int Ns, int... Rs>
 struct TwPowCountImpl;
@@ -514,6 +518,30 @@ struct Twiddles<N, C, TW_LAST> {
     }
 };
 
+template <int N, class C>
+struct Twiddles<N, C, TW_SPLIT> {
+    static constexpr int COUNT = TwPowCountOf<N, RadicesOf<N>>::value > 0 ? 6 * TwPowCountOf<N, RadicesOf<N>>::value : 1;
+    C w[COUNT];  // group g: w[6 g .. 6 g + 2] = w^1..w^3, w[6 g + 3 .. 6 g + 5] = w^4, w^8, w^12
+    __device__ __forceinline__ void launder() {}
+    template <int TwOff, int RegOff, int PowOff, int R, int Ns, bool INV>
+    __device__ __forceinline__ void apply(C* u, int k, int) const {
+        static_assert(R == 16, "TW_SPLIT serves radix-16 passes");
+        const int g = 6 * (PowOff + k);
+        static_for<R - 1>([&](auto rc) {
+            constexpr int r = decltype(rc)::value + 1;
+            constexpr int a = r / 4, b = r % 4;
+            C t;
+            if constexpr (a == 0)
+                t = w[g + b - 1];
+            else if constexpr (b == 0)
+                t = w[g + 2 + a];
+            else
+                t = cmul(w[g + 2 + a], w[g + b - 1]);
+            u[r] = INV ? cmulc(u[r], t) : cmul(u[r], t);
+        });
+    }
+};
+
 template <int N, class C, int MODE, int E, int Ns, int TwOff, int RegOff, int PowOff, int R, int... Rest>
 __device__ __forceinline__ void load_twiddles_pass(Twiddles<N, C, MODE>& tw, int t, const C* __restrict__ table) {
     constexpr int T = PlanOf<N>::T;  // N is the plan key here
@@ -526,6 +554,14 @@ __device__ __forceinline__ void load_twiddles_pass(Twiddles<N, C, MODE>& tw, int
                 static_for<R - 1>([&](auto rc) {
                     constexpr int r = decltype(rc)::value;
                     tw.w[RegOff + k * (R - 1) + r] = table[TwOff + r * Ns + j];
+                });
+            } else if constexpr (MODE == TW_SPLIT) {
+                static_assert(R == 16, "TW_SPLIT serves radix-16 passes");
+                const int g = 6 * (PowOff + k);
+                static_for<3>([&](auto bc) {
+                    constexpr int b = decltype(bc)::value + 1;
+                    tw.w[g + b - 1] = table[TwOff + (b - 1) * Ns + j];      // w^b
+                    tw.w[g + 2 + b] = table[TwOff + (4 * b - 1) * Ns + j];  // w^(4b)
                 });
             } else if constexpr (MODE == TW_LAST) {
                 if constexpr (sizeof...(Rest) == 0) {

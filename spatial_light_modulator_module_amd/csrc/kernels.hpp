@@ -118,8 +118,11 @@ enum ColMode : int {
 };
 
 // target element types: 0 = uint8 (amplitude rounded to float16 as numpy's
-// sqrt(uint8) does), 1 = float32 (amplitude = sqrtf).
-enum TgtType : int { TGT_U8 = 0, TGT_F32 = 1, TGT_NUM = 2 };
+// sqrt(uint8) does), 1 = float32 (amplitude = sqrtf),
+// 2 = float32 amplitude a_T = sqrtf(T) already (the device copy of a float32
+// target in GS plans: set_target takes the square root once, the iteration
+// kernels read a_T and form T = a_T^2 only for the error statistics).
+enum TgtType : int { TGT_U8 = 0, TGT_F32 = 1, TGT_AMP = 2, TGT_NUM = 3 };
 
 using RowFn = void (*)(RowParams);
 using ColFn = void (*)(ColParams);
@@ -497,6 +500,7 @@ struct TgtLoad<TGT_U8> {
     __device__ __forceinline__ static float amp(float t) {
         return __half2float(__float2half_rn(__builtin_amdgcn_sqrtf(t)));
     }
+    __device__ __forceinline__ static float intensity(float t) { return t; }
 };
 template <>
 struct TgtLoad<TGT_F32> {
@@ -510,6 +514,18 @@ struct TgtLoad<TGT_F32> {
         const float c = fmaf(r, 0.5f * y, s);
         return (t >= 1.17549435e-38f && t <= 3.40282347e38f) ? c : __builtin_amdgcn_sqrtf(t);
     }
+    __device__ __forceinline__ static float intensity(float t) { return t; }
+};
+// The statistics' T from a_T: a_T^2 is within 2^-23 of T relative (one
+// correctly rounded square root, one rounded square), so sum E T moves by
+// ~1e-7 / sqrt(pixels) relative: far inside the error curves' 1e-4 gates.
+template <>
+struct TgtLoad<TGT_AMP> {
+    __device__ __forceinline__ static float load(const void* p, long long i) {
+        return static_cast<const float*>(p)[i];
+    }
+    __device__ __forceinline__ static float amp(float a) { return a; }
+    __device__ __forceinline__ static float intensity(float a) { return a * a; }
 };
 
 // Wave reductions of doubles without the LDS pipe (-DSLM_DPP_REDUCE=0: __shfl_xor
@@ -1159,7 +1175,7 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P, M
         }
     };
     auto ld_tgt = [&](long long idx, float (&tv)[L][NT], int m) {
-        if constexpr (L == 2 && TT == TGT_F32) {
+        if constexpr (L == 2 && (TT == TGT_F32 || TT == TGT_AMP)) {
             const float2 q = *reinterpret_cast<const float2*>(static_cast<const float*>(p.tgt) + idx);
             tv[0][m] = q.x;
             tv[1][m] = q.y;
@@ -1362,17 +1378,34 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P, M
         } else {
             double mx = 0.0, s2 = 0.0, st = 0.0;
             const S norm = (MODE == COL_GD_GRAD) ? (S)p.norm[b] : (S)0;
+            // GS: the launch of the run's last iteration (every iteration of a
+            // checked run) also stores E = |C|^2, the expected output of
+            // src/algorithms.py:36, in layout Y (e_blk; relayouted to row-major
+            // after the run) -- no separate forward transform for it
+            float* const e_blk = MODE == COL_GS_MAIN ? p.e_blk : nullptr;
+            const long long eb = MODE == COL_GS_MAIN ? out_base(b, wg) : 0;
+            // GS: the thread's partial sums in float32 (its E elements of one
+            // column), folded across the workgroup in float64: a few 1e-7 of a
+            // partial, averaging out over the hologram's partials (the error's
+            // expansion cancels by ~1e2 late in a run: error curves still
+            // agree to ~1e-6 relative, gated at 1e-4)
+            float mxf = 0.f, s2f = 0.f, stf = 0.f;
             auto epi = [&](int l, int m, C& z) {
                 const S e = z.x * z.x + z.y * z.y;
                 const float tl = tv[l][m];
-                if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_STATS) {
-                    // |C|^2 as the reference's float64 expected_outcome sees it
+                if constexpr (MODE == COL_GS_MAIN) {
+                    const float ef = (float)e;  // |C|^2 as the reference's float64 expected_outcome sees it
+                    mxf = fmaxf(mxf, ef);
+                    s2f = fmaf(ef, ef, s2f);
+                    stf = fmaf(ef, TgtLoad<TT>::intensity(tl), stf);
+                } else if constexpr (MODE == COL_GD_STATS) {
                     const double ed = (double)(float)e;
                     mx = fmax(mx, ed);
                     s2 += ed * ed;
                     st += ed * (double)tl;
                 }
                 if constexpr (MODE == COL_GS_MAIN) {
+                    if (e_blk) e_blk[eb + m * kStepY + l] = (float)e;
                     z = unit_scale(z, (S)TgtLoad<TT>::amp(tl));  // D = a_T C/|C| (src/algorithms.py:33)
                 } else if constexpr (MODE == COL_GD_GRAD) {
                     // mask * F * (output - T), output = |F|^2 norm / max (src/algorithms.py:80,85-88)
@@ -1397,6 +1430,11 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P, M
             trace_point(trace, tile, 2, false);
             if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_GRAD) st_tile(out_base(b, wg), v);
             // the cross-lane statistics reduction (LDS only) runs while the field stores drain
+            if constexpr (MODE == COL_GS_MAIN) {
+                mx = mxf;
+                s2 = s2f;
+                st = stf;
+            }
             if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_STATS) {
                 block_reduce_stats<THREADS>(mx, s2, st);
                 if (threadIdx.x == 0) {
@@ -1488,6 +1526,45 @@ __global__ void __launch_bounds__(256) field_phase_kernel(const float2* field, f
         const int y = (int)(r / W), x = (int)(r - (long long)y * W);
         const float2 f = field[b * holo + blk_index<PLOG>(y, x, H)];
         phase[i] = atan2f(f.y, f.x);
+    }
+}
+
+// blocked layout -> row-major for float planes (the expected output), through
+// an LDS tile of 64 x 64: the reads are whole panel runs (64 rows x P floats
+// contiguous per panel), the writes 256-B row segments. grid (W / 64, H / 64,
+// B), 256 threads; H and W are multiples of 64 for every supported side.
+template <int PLOG>
+__global__ void __launch_bounds__(256) unblock_tile_kernel(const float* in, float* out, int H, int W) {
+    constexpr int P = 1 << PLOG;
+    __shared__ float tile[64][65];
+    const long long holo = (long long)H * W;
+    const int x0 = blockIdx.x * 64, y0 = blockIdx.y * 64;
+    const float* src = in + blockIdx.z * holo;
+    float* dst = out + blockIdx.z * holo;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int i = threadIdx.x + 256 * k;  // panel-major order of the tile: (q, yy, xx)
+        const int xx = i & (P - 1), yy = (i >> PLOG) & 63, q = i >> (PLOG + 6);
+        tile[yy][q * P + xx] = src[(((long long)(x0 >> PLOG) + q) * H + y0 + yy) * P + xx];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int i = threadIdx.x + 256 * k;
+        const int yy = i >> 6, xx = i & 63;
+        dst[(long long)(y0 + yy) * W + x0 + xx] = tile[yy][xx];
+    }
+}
+
+// float32 target (row-major) -> its amplitude sqrt(T) in the blocked layout
+// (GS plans keep a_T on the device: TGT_AMP), the square root of TgtLoad<TGT_F32>
+template <int PLOG>
+__global__ void __launch_bounds__(256) amp_blocked_kernel(const float* in, float* out, long long n, int H, int W) {
+    const long long holo = (long long)H * W;
+    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+        const long long b = i / holo, r = i - b * holo;
+        const int y = (int)(r / W), x = (int)(r - (long long)y * W);
+        out[b * holo + blk_index<PLOG>(y, x, H)] = TgtLoad<TGT_F32>::amp(in[i]);
     }
 }
 

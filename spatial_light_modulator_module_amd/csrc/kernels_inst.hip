@@ -37,10 +37,13 @@ ColFn col_table_cw(int mode, int tt) {
     } else {
         const bool u8 = (tt == TGT_U8);
         switch (mode) {
-            case COL_GS_MAIN:
-                return u8 ? col_kernel<N, CW, COL_GS_MAIN, TGT_U8, P, LID> : col_kernel<N, CW, COL_GS_MAIN, TGT_F32, P, LID>;
+            case COL_GS_MAIN:  // GS plans hold a float32 target as its amplitude (TGT_AMP)
+                return u8 ? col_kernel<N, CW, COL_GS_MAIN, TGT_U8, P, LID>
+                          : tt == TGT_AMP ? col_kernel<N, CW, COL_GS_MAIN, TGT_AMP, P, LID> : nullptr;
             case COL_REAL_INV:
-                return u8 ? col_kernel<N, CW, COL_REAL_INV, TGT_U8, P, LID> : col_kernel<N, CW, COL_REAL_INV, TGT_F32, P, LID>;
+                return u8 ? col_kernel<N, CW, COL_REAL_INV, TGT_U8, P, LID>
+                          : tt == TGT_AMP ? col_kernel<N, CW, COL_REAL_INV, TGT_AMP, P, LID>
+                                          : col_kernel<N, CW, COL_REAL_INV, TGT_F32, P, LID>;
             case COL_GD_STATS:
                 return u8 ? col_kernel<N, CW, COL_GD_STATS, TGT_U8, P, LID> : col_kernel<N, CW, COL_GD_STATS, TGT_F32, P, LID>;
             case COL_GD_GRAD:

@@ -150,6 +150,18 @@ int get_twiddles(int pk, int prec, const void** out) {
     return 0;
 }
 
+// Holds a stream for `ticks` of the 100 MHz s_memrealtime clock (one wave,
+// bounded by time alone). slm_plan_run_timed queues it first so the host
+// enqueues every launch of the timed run while it waits: the timed kernels then
+// run back to back, as in the replayed graph of slm_plan_run, instead of each
+// starting on an idle device behind the host's per-launch enqueue cost (which
+// measured up to 0.5 us shorter per 1024^2 launch than the same kernel in the
+// graph, profiles/r04).
+__global__ void __launch_bounds__(64) hold_kernel(unsigned long long ticks) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+
 __global__ void fill_int_kernel(int* p, int n, int v) {
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = v;
 }
@@ -250,6 +262,7 @@ int relayout(int plog, const V* in, V* out, long long n, int H, int W, bool to_b
         case 1: relayout_launch<1>(in, out, n, H, W, to_blocked, st); break;
         case 2: relayout_launch<2>(in, out, n, H, W, to_blocked, st); break;
         case 3: relayout_launch<3>(in, out, n, H, W, to_blocked, st); break;
+        case 4: relayout_launch<4>(in, out, n, H, W, to_blocked, st); break;
         default: return fail(SLM_ERR_UNSUPPORTED, "no relayout for panel log2 %d", plog);
     }
     HIP_TRY(hipGetLastError());
@@ -263,6 +276,7 @@ enum GdMode : int { GD_AUTO = 0, GD_LIN = 1, GD_FUSED = 2, GD_TWO = 3 };
 
 struct slm_plan {
     int algo = 0, B = 0, H = 0, W = 0, tt = 1, has_ain = 0, max_loops = 0;
+    int dev_tt = 1;  // TgtType of the device target buffer: tt, or TGT_AMP for float32 GS targets
     int cw = 4, nwg = 0, col_threads = 0, row_threads = 0, rpw = 0;
     int row_key = -1, col_key = -1;  // radix plans (kPlans) of the row / column transforms
     int lid = -1;                    // blocked layout pair (LayoutId), fixed at the first configure
@@ -336,6 +350,7 @@ struct slm_plan {
     // enqueue_run captured once per (loops, tol, checked, wa, warm-start state)
     // and relaunched as one graph -- 3 % per 1024^2 GS iteration, 6 % at 256^2
     // (gpurun_out/exp17: the inter-kernel gaps of 400 dependent launches)
+    hipEvent_t marks[2] = {nullptr, nullptr};  // slm_plan_mark stopwatch
     hipGraphExec_t gexec = nullptr;
     int g_loops = -1, g_checked = -1, g_state = -1;
     double g_tol = 0.0;
@@ -352,22 +367,22 @@ namespace {
 int pick_cw(int ck, int W) {
     if (const char* s = std::getenv("SLM_COL_CW")) {
         const int cw = std::atoi(s);
-        if (col_fn(ck, cw, COL_GS_MAIN, TGT_F32, PREC_F32) && W % cw == 0) return cw;
+        if (col_fn(ck, cw, COL_GS_MAIN, TGT_AMP, PREC_F32) && W % cw == 0) return cw;
     }
     // narrow plans (a single small image) take 2-column tiles: twice the
     // workgroups per CU, the partner tile reads the other half of each line
     // through the same XCD's L2 (measured 13.0 -> 10.7 us per 1024^2 pass)
-    if (kPlans[ck].variant == 1 && W % 2 == 0 && col_fn(ck, 2, COL_GS_MAIN, TGT_F32, PREC_F32)) return 2;
+    if (kPlans[ck].variant == 1 && W % 2 == 0 && col_fn(ck, 2, COL_GS_MAIN, TGT_AMP, PREC_F32)) return 2;
     // first tile (in this order) whose complex64 LDS leaves room for two
     // workgroups per CU; 2-column tiles only with >= 8 waves (long columns)
     for (int cw : {4, 8, 16, 2}) {
-        if (W % cw || !col_fn(ck, cw, COL_GS_MAIN, TGT_F32, PREC_F32)) continue;
+        if (W % cw || !col_fn(ck, cw, COL_GS_MAIN, TGT_AMP, PREC_F32)) continue;
         const long long lds = (long long)lds_line(kPlans[ck].n) * cw * 8;
         const int threads = cw * (kPlans[ck].n / kPlans[ck].e);
         if (lds <= 80 * 1024 && (cw != 2 || threads >= 512)) return cw;
     }
     for (int cw : {4, 8, 16, 2})
-        if (W % cw == 0 && col_fn(ck, cw, COL_GS_MAIN, TGT_F32, PREC_F32)) return cw;
+        if (W % cw == 0 && col_fn(ck, cw, COL_GS_MAIN, TGT_AMP, PREC_F32)) return cw;
     return 0;
 }
 
@@ -430,7 +445,7 @@ int configure(slm_plan* p, int prec) {
     const char* gl = std::getenv("SLM_GD_LAYOUT");
     const bool algo_ok = p->algo == SLM_ALGO_GS || !(gl && !std::strcmp(gl, "default"));
     const bool narrow_ok = algo_ok && row_fn(row_key, ROW_GS_MAIN, prec, LAYOUT_NARROW) &&
-                           col_fn(col_key, cw, COL_GS_MAIN, TGT_F32, prec, LAYOUT_NARROW);
+                           col_fn(col_key, cw, COL_GS_MAIN, TGT_AMP, prec, LAYOUT_NARROW);
     const char* ls = std::getenv("SLM_LAYOUT");
     if (narrow_ok && !(ls && !std::strcmp(ls, "default"))) lid = LAYOUT_NARROW;
     if (p->lid >= 0 && lid != p->lid) {
@@ -559,7 +574,7 @@ int launch_row(slm_plan* p, int mode, const RowParams& rp, int cls) {
 }
 
 int launch_col(slm_plan* p, int mode, const ColParams& cp, int cls) {
-    const int tt = (mode == COL_EXPECTED || mode == COL_FFT_FWD || mode == COL_FFT_INV) ? TGT_F32 : p->tt;
+    const int tt = (mode == COL_EXPECTED || mode == COL_FFT_FWD || mode == COL_FFT_INV) ? TGT_F32 : p->dev_tt;
     ColFn fn = col_fn(p->col_key, p->cw, mode, tt, p->prec, p->lid);
     if (!fn) return fail(SLM_ERR_UNSUPPORTED, "no column kernel for height %d cw %d mode %d", p->H, p->cw, mode);
     ColParams c = cp;
@@ -570,14 +585,26 @@ int launch_col(slm_plan* p, int mode, const ColParams& cp, int cls) {
     return launch(p, cls, fn, dim3(grid), dim3(p->col_threads), c);
 }
 
-// expected output |C|^2 (src/algorithms.py:36): the column kernel writes it in
-// layout Y into the free Y buffer (every reader of Y precedes this on the
-// stream), then one relayout to the row-major e_out
+// the expected output E written by the GS column pass in layout Y (e_blk) ->
+// the row-major e_out (LDS-tiled transpose; one launch for the batch)
+int unblock_expected(slm_plan* p, const float* e_blk) {
+    const dim3 grid(p->W / 64, p->H / 64, p->B);
+    switch (layout_y_log2(p->lid)) {
+        case 1: return launch(p, SLM_KERNEL_OTHER, unblock_tile_kernel<1>, grid, dim3(256), e_blk, p->e_out, p->H, p->W);
+        case 2: return launch(p, SLM_KERNEL_OTHER, unblock_tile_kernel<2>, grid, dim3(256), e_blk, p->e_out, p->H, p->W);
+        case 3: return launch(p, SLM_KERNEL_OTHER, unblock_tile_kernel<3>, grid, dim3(256), e_blk, p->e_out, p->H, p->W);
+        case 4: return launch(p, SLM_KERNEL_OTHER, unblock_tile_kernel<4>, grid, dim3(256), e_blk, p->e_out, p->H, p->W);
+        default: return fail(SLM_ERR_UNSUPPORTED, "no unblock kernel for panel log2 %d", layout_y_log2(p->lid));
+    }
+}
+
+// expected output |C|^2 (src/algorithms.py:36) of GD (and the intensity
+// helper): a forward column pass writes it in layout Y into the free Y buffer
+// (every reader of Y precedes this on the stream), then the tiled unblock
 int launch_expected(slm_plan* p, ColParams cp) {
     cp.e_blk = reinterpret_cast<float*>(p->y);
     RC(launch_col(p, COL_EXPECTED, cp, SLM_KERNEL_OTHER));
-    return relayout(layout_y_log2(p->lid), (const float*)p->y, p->e_out, (long long)p->B * p->holo, p->H, p->W,
-                    false, p->stream);
+    return unblock_expected(p, reinterpret_cast<const float*>(p->y));
 }
 
 StatsParams stats_params(slm_plan* p, double tol) {
@@ -619,10 +646,17 @@ int enqueue_gs(slm_plan* p, int loops, double tol, int checked) {
         rp.iter = -1;
         RC(launch_row(p, ROW_GS_MAIN, rp, SLM_KERNEL_OTHER));
     }
+    // expected_outcome = |C|^2 of the last iteration (src/algorithms.py:36): the
+    // column pass of the last iteration (of every iteration in a checked run,
+    // where the last is not known in advance; a stopped hologram's later passes
+    // leave it untouched) stores it in layout Y into phase_out, free until the
+    // phase extraction below
+    float* const e_blk = p->phase_out;
     for (int i = 0; i < loops; ++i) {
         cp.in = p->xa;
         cp.out = p->y;
         cp.iter = i;
+        cp.e_blk = (checked || i + 1 == loops) ? e_blk : nullptr;
         RC(launch_col(p, COL_GS_MAIN, cp, SLM_KERNEL_COL_MAIN));
         if (checked) RC(launch_finalize(p, tol, i));
         if (i + 1 < loops) {
@@ -632,12 +666,10 @@ int enqueue_gs(slm_plan* p, int loops, double tol, int checked) {
             RC(launch_row(p, ROW_GS_MAIN, rp, SLM_KERNEL_ROW_MAIN));
         }
     }
-    // hologram = np.angle(A) (src/algorithms.py:48); expected_outcome = |C|^2 (:36)
+    RC(unblock_expected(p, e_blk));
+    // hologram = np.angle(A) (src/algorithms.py:48)
     rp.in = p->y;
     RC(launch_row(p, ROW_GS_PHASE, rp, SLM_KERNEL_OTHER));
-    cp.in = p->xa;
-    cp.in_alt = p->xa;
-    RC(launch_expected(p, cp));
     return 0;
 }
 
@@ -731,8 +763,9 @@ int enqueue_gd(slm_plan* p, int loops, double tol, int checked, float wa) {
     {
         const long long n = (long long)p->B * p->holo;
         const int grid = (int)std::min<long long>(4096, (n + 255) / 256);
-        auto fk = layout_y_log2(p->lid) == 1 ? field_phase_kernel<1>
-                  : layout_y_log2(p->lid) == 3 ? field_phase_kernel<3> : field_phase_kernel<2>;
+        const int yl = layout_y_log2(p->lid);
+        auto fk = yl == 1 ? field_phase_kernel<1>
+                  : yl == 3 ? field_phase_kernel<3> : yl == 4 ? field_phase_kernel<4> : field_phase_kernel<2>;
         RC(launch(p, SLM_KERNEL_OTHER, fk, dim3(grid), dim3(256), (const float2*)p->field, p->phase_out, n, p->H,
                   p->W));
     }
@@ -801,6 +834,8 @@ void free_plan(slm_plan* p) {
         (void)hipEventDestroy(e.second);
     }
     if (p->gexec) (void)hipGraphExecDestroy(p->gexec);
+    for (hipEvent_t e : p->marks)
+        if (e) (void)hipEventDestroy(e);
     if (p->stream) (void)hipStreamDestroy(p->stream);
     delete p;
 }
@@ -919,6 +954,8 @@ int plan_create_on(int device, int algo, int batch, int height, int width, int t
     p->H = height;
     p->W = width;
     p->tt = tgt_type;
+    // GS keeps a float32 target as its amplitude on the device (set_target)
+    p->dev_tt = (algo == SLM_ALGO_GS && tgt_type == SLM_TGT_F32) ? TGT_AMP : tgt_type;
     p->has_ain = has_ain ? 1 : 0;
     p->max_loops = max_loops;
     p->device = device;
@@ -1032,6 +1069,9 @@ int slm_plan_set_target(slm_plan* p, const void* tgt) {
     const long long n = (long long)p->B * p->holo;
     const size_t tb = p->tt == SLM_TGT_U8 ? 1 : 4;
     void* stage = p->e_out;  // n floats >= n target elements of either type
+    // host arrays stay pageable: HIP's staged copies run at ~45 GB/s for a 4 MB
+    // target here; pinning the caller's buffer or a pinned staging buffer plus a
+    // host memcpy measured no faster (tools/xfer_probe.py)
     HIP_TRY(hipMemcpyAsync(stage, tgt, (size_t)n * tb, hipMemcpyHostToDevice, p->stream));
     const int nblk = ts_blocks(p->holo);
     if (p->tt == SLM_TGT_U8) {
@@ -1041,7 +1081,16 @@ int slm_plan_set_target(slm_plan* p, const void* tgt) {
     } else {
         hipLaunchKernelGGL(target_stats_partial_kernel<float>, dim3(nblk, p->B), dim3(kTsThreads), 0, p->stream,
                            (const float*)stage, p->holo, p->ts_part);
-        RC(relayout(layout_x_log2(p->lid), (const float*)stage, (float*)p->tgt, n, p->H, p->W, true, p->stream));
+        if (p->dev_tt == TGT_AMP) {
+            const int grid = (int)std::min<long long>(8192, (n + 255) / 256);
+            const int xl = layout_x_log2(p->lid);
+            auto k = xl == 1 ? amp_blocked_kernel<1> : xl == 3 ? amp_blocked_kernel<3>
+                     : xl == 4 ? amp_blocked_kernel<4> : amp_blocked_kernel<2>;
+            hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, p->stream, (const float*)stage, (float*)p->tgt, n, p->H,
+                               p->W);
+        } else {
+            RC(relayout(layout_x_log2(p->lid), (const float*)stage, (float*)p->tgt, n, p->H, p->W, true, p->stream));
+        }
     }
     hipLaunchKernelGGL(target_stats_final_kernel, dim3(p->B), dim3(kTsThreads), 0, p->stream, p->ts_part, nblk,
                        p->norm, p->normf, p->sum_t2);
@@ -1165,6 +1214,19 @@ int slm_plan_run(slm_plan* p, int loops, double tol, int checked, float wa) {
 
 int slm_plan_run_timed(slm_plan* p, int loops, double tol, int checked, float wa, double* us, int* counts) {
     if (!p) return fail(SLM_ERR_ARG, "null plan");
+    // $SLM_TIMED_HOLD: 100 MHz ticks of hold per launch of the run (0 = no hold)
+    static const long long hold = [] {
+        const char* e = std::getenv("SLM_TIMED_HOLD");
+        return e ? std::atoll(e) : 1000LL;
+    }();
+    if (hold > 0) {
+        // ~10 us of host enqueue per launch of the run, at most 0.2 s
+        const long long launches = 2LL * loops + 16;
+        const unsigned long long ticks = (unsigned long long)std::min<long long>(launches * hold, 20000000LL);
+        HIP_TRY(hipSetDevice(p->device));
+        hipLaunchKernelGGL(hold_kernel, dim3(1), dim3(64), 0, p->stream, ticks);
+        HIP_TRY(hipGetLastError());
+    }
     p->timing = true;
     p->ev_used = 0;
     int rc = enqueue_run(p, loops, tol, checked, wa);
@@ -1202,6 +1264,24 @@ int slm_plan_sync(slm_plan* p) {
 }
 
 int slm_plan_gd_recoveries(slm_plan* p) { return p ? p->gd_recoveries : -1; }
+
+int slm_plan_mark(slm_plan* p, int which) {
+    if (!p || which < 0 || which > 1) return fail(SLM_ERR_ARG, "bad mark arguments");
+    HIP_TRY(hipSetDevice(p->device));
+    if (!p->marks[which]) HIP_TRY(hipEventCreate(&p->marks[which]));
+    HIP_TRY(hipEventRecord(p->marks[which], p->stream));
+    return 0;
+}
+
+int slm_plan_marked_ms(slm_plan* p, double* ms) {
+    if (!p || !ms) return fail(SLM_ERR_ARG, "null argument");
+    if (!p->marks[0] || !p->marks[1]) return fail(SLM_ERR_STATE, "record marks 0 and 1 first");
+    HIP_TRY(hipEventSynchronize(p->marks[1]));
+    float t = 0.f;
+    HIP_TRY(hipEventElapsedTime(&t, p->marks[0], p->marks[1]));
+    *ms = t;
+    return 0;
+}
 
 int slm_plan_read(slm_plan* p, float* phase, float* expected, double* stats, int* iters) {
     if (!p) return fail(SLM_ERR_ARG, "null plan");

@@ -31,6 +31,12 @@ class _FakePlan:
     def sync(self):
         pass
 
+    def mark(self, which):
+        pass
+
+    def marked_ms(self):
+        return 3.0 * 3.4  # 3 steps of ~3.4 ms
+
     def gather_phase(self, counts, root=0, host_out=None):
         if host_out is not None:
             host_out[:] = 0.5
@@ -142,7 +148,8 @@ def test_bench_two_ranks_json_shape(tmp_path):
     assert out["value"] > 0 and out["check"] == "ok"
     assert "cpu_baseline" not in out  # rank 0 at N = 1 only
     r = out["roofline"]
-    assert {"frac", "frac_physical", "achieved", "peak", "traffic"} <= set(r)
+    assert {"frac", "frac_physical", "achieved", "peak", "traffic", "event_avg_us", "in_graph_scale"} <= set(r)
+    assert r["avg_us"] > r["event_avg_us"]  # 3.4 ms per step against 3.1 ms of per-launch events
     ranks = out["ranks"]
     assert [d["rank"] for d in ranks] == [0, 1]
     assert [d["device"] for d in ranks] == [0, 1] and ranks[1]["pci_bus_id"] == "0000:01:00.0"

@@ -146,3 +146,29 @@ def test_run_gs_multi_exact_stats_frames(gpu):
         np.testing.assert_array_equal(norm, rnorm)
         for a, b in zip(errs, rerrs):
             np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.gpu
+def test_multi_gpu_diagnostics(gpu):
+    """slm_gs_multi_timing reports one (wall, run) pair per shard of the last
+    slm_gs_multi (empty shards 0), slm_plan_time_gather times the phase gather
+    on its own (the root sends nothing), slm_plan_device / slm_device_pci_bus_id
+    name the GPU: the per-rank record bench.py prints at N > 1."""
+    lib = gpu
+    t = _targets(5, 128, False)
+    lib.gs_multi(t, 6, [0, 0, 0, 0, 0, 0, 0])
+    wall, run = lib.gs_multi_timing()
+    assert len(wall) == len(run) == 7
+    for k, (w, r) in enumerate(zip(wall, run)):
+        if k < 5:
+            assert w >= r > 0
+        else:
+            assert w == r == 0  # 7 shards of a 5-batch: two are empty
+    with lib.Plan(lib.ALGO_GS, 5, 128, 128, lib.TGT_F32, False, 6) as p:
+        p.set_target(t)
+        p.run(6)
+        ms, nbytes = p.time_gather([5], root=0, reps=3)
+        assert ms >= 0 and nbytes == 0
+        assert p.device == 0
+    bus = lib.pci_bus_id(0)
+    assert len(bus) >= 7 and ":" in bus

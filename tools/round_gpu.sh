@@ -10,7 +10,7 @@ out=gpurun_out/$tag
 mkdir -p $out
 repo=$(pwd)
 if [ "$2" != "skip-tests" ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $out/pytest_gpu.log 2>&1 || { echo "pytest failed rc=$?"; tail -30 $out/pytest_gpu.log; exit 1; }
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rP --timeout 300 --timeout-method thread > $out/pytest_gpu.log 2>&1 || { echo "pytest failed rc=$?"; tail -30 $out/pytest_gpu.log; exit 1; }
   tail -3 $out/pytest_gpu.log
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 || { echo "smoke failed rc=$?"; tail -30 $out/smoke.log; exit 1; }
   tail -3 $out/smoke.log
