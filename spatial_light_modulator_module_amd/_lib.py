@@ -33,6 +33,8 @@ KERNEL_OTHER = 3
 NUM_KERNEL_CLASSES = 4
 KERNEL_CLASS_NAMES = ("col_main", "row_main", "gd_stats", "other")
 
+# sides with a radix plan (the fused FFT kernels); any other side runs the
+# DFT-GEMM engine (generic.hip)
 SUPPORTED_LENGTHS = (64, 128, 256, 512, 768, 1024, 2048, 4096)
 
 
@@ -342,10 +344,12 @@ class Plan:
 
     def engine(self) -> tuple[str, str]:
         """(column, row) transform engine of the GS iteration kernels:
-        "stockham" or "shuffle" (wave-shuffle pair, fft_shuffle.hpp)."""
+        "stockham", "shuffle" (wave-shuffle pair, fft_shuffle.hpp) or, for
+        sides without a radix plan, "dft-gemm" (float64 DFT matrices on
+        rocBLAS ZGEMM, generic.hip)."""
         c, r = ctypes.c_int(), ctypes.c_int()
         check(self._lib.slm_plan_engine(self.handle, ctypes.byref(c), ctypes.byref(r)), "slm_plan_engine")
-        names = ("stockham", "shuffle")
+        names = ("stockham", "shuffle", "dft-gemm")
         return names[c.value], names[r.value]
 
     def layout(self) -> tuple[int, int]:

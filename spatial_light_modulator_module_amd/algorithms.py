@@ -9,13 +9,14 @@ error_evolution)`` triple (float64 arrays and a list of np.float64). All
 iteration arithmetic runs in libslm_hip.so; this module only prepares inputs
 (dtype rules, initial guesses) and formats results.
 
-Differences that remain: image sides must be one of
-SUPPORTED_LENGTHS, and the loop state lives in complex64 in HBM with float32
+Differences that remain: for image sides in SUPPORTED_LENGTHS
+(the fused FFT kernels) the loop state lives in complex64 in HBM with float32
 butterflies, twiddles and projections by default (float64 butterflies per plan
 with Plan.set_precision or $SLM_PRECISION=f64), so phases match the float64
 reference to <= 1e-5 rms under the warm-start protocol of SURVEY.md 8c (float32
 margins measured in DESIGN.md section 5: 4.0e-6..6.0e-6 at 256^2-1024^2), not
-bitwise. A float64 target is carried as float32 on the device, with its max
+bitwise; any other shape runs the float64 DFT-GEMM engine (complex128
+state). A float64 target is carried as float32 on the device, with its max
 and sum of squares (the error's constant terms) kept exact in float64.
 """
 from __future__ import annotations
@@ -27,7 +28,7 @@ import sys
 import numpy as np
 
 from . import _lib
-from ._lib import ALGO_GD, ALGO_GS, SUPPORTED_LENGTHS, TGT_F32, TGT_U8
+from ._lib import ALGO_GD, ALGO_GS, TGT_F32, TGT_U8
 
 # ---------------------------------------------------------------------------
 # input preparation (reference dtype rules)
@@ -35,14 +36,15 @@ from ._lib import ALGO_GD, ALGO_GS, SUPPORTED_LENGTHS, TGT_F32, TGT_U8
 
 
 def _check_shape(t: np.ndarray):
+    """Any (h, w), as the reference (src/algorithms.py:20-27): sides in
+    SUPPORTED_LENGTHS run the fused FFT kernels, every other shape the
+    float64 DFT-GEMM engine (csrc/generic.hip)."""
     if t.ndim != 2:
         # the reference unpacks `w, l = demanded_output.shape` (src/algorithms.py:20)
         raise ValueError(f"too many values to unpack (expected 2): target has shape {t.shape}")
     h, w = t.shape
-    if h not in SUPPORTED_LENGTHS or w not in SUPPORTED_LENGTHS:
-        raise ValueError(
-            f"image shape {t.shape} is not supported by the MI355X path: each side must be one of "
-            f"{SUPPORTED_LENGTHS} (the reference CLI resizes to 768x1024)")
+    if h < 1 or w < 1:
+        raise ValueError(f"empty target of shape {t.shape}")
     return h, w
 
 

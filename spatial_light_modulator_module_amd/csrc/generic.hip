@@ -1,0 +1,435 @@
+// Any-size engine (generic.hpp): GS / GD iterations whose 2-D transforms are
+// complex float64 products with the DFT matrices, on rocBLAS ZGEMM.
+//
+// Row-major [H][W] images are, to a column-major BLAS, W x H matrices M^T
+// (leading dimension W). With the symmetric DFT matrices F_N[j][k] =
+// exp(-2 pi i jk / N):
+//     fft2(M) = F_H M F_W   <=>   fft2(M)^T = F_W M^T F_H
+// so a forward 2-D transform is T = F_W M^T (m = W, n = H, k = W), then
+// T F_H (m = W, n = H, k = H); the inverse (unscaled) takes the conjugate
+// transposes, which are the conjugates: op = rocblas_operation_conjugate_transpose.
+// Every hologram of the batch shares the matrices (stride 0 in the batched
+// product). ZGEMM runs with atomics disabled, so a product of the same
+// operands is the same bits every time (a stopped hologram of a checked run is
+// frozen by leaving its inputs untouched, see enqueue).
+//
+// Numerics follow the reference's float64 path (src/algorithms.py:10-49,
+// 60-112): complex128 state, float64 statistics (E = |C|^2 unrounded),
+// amplitudes as numpy forms them (sqrt(uint8) -> float16, sqrt(float32) ->
+// float32), the cold start's ifft2 of a float amplitude rounded to complex64.
+#include <rocblas/rocblas.h>
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "../../include/slm_hip.h"
+#include "generic.hpp"
+#include "kernels.hpp"
+
+int slm_set_error(int code, const char* msg);  // slm_capi.hip
+
+namespace slm {
+
+struct GenericEngine {
+    rocblas_handle blas = nullptr;
+    double2* fh = nullptr;   // F_H [H][H]
+    double2* fw = nullptr;   // F_W [W][W] (== fh for square images)
+    double2* a = nullptr;    // GS: A; GD: the inverse-transformed gradient g
+    double2* b = nullptr;    // GS: B, then C in place; GD: u, then F in place
+    double2* d = nullptr;    // GS: D; GD: G
+    double2* x = nullptr;    // GD: the field x
+    double2* tmp = nullptr;  // product intermediate
+};
+
+namespace {
+
+constexpr int kGT = 256;  // threads per block of the element-wise kernels
+
+#define G_HIP(expr)                                                                      \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess) return slm_set_error(SLM_ERR_HIP, hipGetErrorString(e_));  \
+    } while (0)
+#define G_BLAS(expr)                                                                     \
+    do {                                                                                 \
+        rocblas_status s_ = (expr);                                                      \
+        if (s_ != rocblas_status_success) return slm_set_error(SLM_ERR_HIP, rocblas_status_to_string(s_)); \
+    } while (0)
+
+int grid_of(long long n) { return (int)std::min<long long>(16384, (n + kGT - 1) / kGT); }
+
+// numpy's amplitude of the target: sqrt(uint8) is float16,
+// sqrt(float32) float32; then widened (the loop multiplies it with complex128)
+__device__ __forceinline__ double g_amp(const void* tgt, int tt, long long i) {
+    if (tt == TGT_U8) return (double)TgtLoad<TGT_U8>::amp(TgtLoad<TGT_U8>::load(tgt, i));
+    return (double)(float)sqrt((double)static_cast<const float*>(tgt)[i]);
+}
+__device__ __forceinline__ double g_t(const void* tgt, int tt, long long i) {
+    return tt == TGT_U8 ? (double)static_cast<const uint8_t*>(tgt)[i] : (double)static_cast<const float*>(tgt)[i];
+}
+__device__ __forceinline__ double g_ain(const float* ain, long long i, long long holo) {
+    return ain ? (double)ain[i % holo] : 1.0;
+}
+// a exp(i angle(z)) == a z / |z|, angle(0) = 0 -> a (src/algorithms.py:30,33)
+__device__ __forceinline__ double2 g_unit(double2 z, double a) {
+    const double n2 = z.x * z.x + z.y * z.y;
+    if (n2 == 0.0) return make_double2(a, 0.0);
+    const double r = a / sqrt(n2);
+    return make_double2(z.x * r, z.y * r);
+}
+
+__global__ void __launch_bounds__(kGT) k_unit(const double2* A, double2* B, const float* ain, long long holo,
+                                              long long n) {
+    for (long long i = blockIdx.x * (long long)kGT + threadIdx.x; i < n; i += (long long)gridDim.x * kGT)
+        B[i] = g_unit(A[i], g_ain(ain, i, holo));
+}
+// warm start: B = a_in exp(1j phi) with exp of a float32 phase in complex64 (numpy)
+__global__ void __launch_bounds__(kGT) k_warm(const float* phi, double2* B, const float* ain, long long holo,
+                                              long long n) {
+    for (long long i = blockIdx.x * (long long)kGT + threadIdx.x; i < n; i += (long long)gridDim.x * kGT) {
+        double s, c;
+        sincos((double)phi[i], &s, &c);
+        const double a = g_ain(ain, i, holo);
+        B[i] = make_double2((double)(float)c * a, (double)(float)s * a);
+    }
+}
+// a_T + 0i (the cold start's ifft2(sqrt(T)) and the "fourier" guess)
+__global__ void __launch_bounds__(kGT) k_amp(const void* tgt, int tt, double2* D, long long n) {
+    for (long long i = blockIdx.x * (long long)kGT + threadIdx.x; i < n; i += (long long)gridDim.x * kGT)
+        D[i] = make_double2(g_amp(tgt, tt, i), 0.0);
+}
+// ifft2 of a float16 / float32 amplitude is complex64 in the reference (src/algorithms.py:27)
+__global__ void __launch_bounds__(kGT) k_round_c64(double2* A, long long n) {
+    for (long long i = blockIdx.x * (long long)kGT + threadIdx.x; i < n; i += (long long)gridDim.x * kGT)
+        A[i] = make_double2((double)(float)A[i].x, (double)(float)A[i].y);
+}
+// "fourier" guess a_in exp(1j angle(ifft2(sqrt T))): angle of complex64 is float32, exp complex64
+// (src/algorithms.py:153-156)
+__global__ void __launch_bounds__(kGT) k_fourier(const double2* A, double2* X, const float* ain, long long holo,
+                                                 long long n) {
+    for (long long i = blockIdx.x * (long long)kGT + threadIdx.x; i < n; i += (long long)gridDim.x * kGT) {
+        const float ang = atan2f((float)A[i].y, (float)A[i].x);
+        double s, c;
+        sincos((double)ang, &s, &c);
+        const double a = g_ain(ain, i, holo);
+        X[i] = make_double2((double)(float)c * a, (double)(float)s * a);
+    }
+}
+__global__ void __launch_bounds__(kGT) k_c64_to_c128(const float2* in, double2* out, long long n) {
+    for (long long i = blockIdx.x * (long long)kGT + threadIdx.x; i < n; i += (long long)gridDim.x * kGT)
+        out[i] = make_double2((double)in[i].x, (double)in[i].y);
+}
+__global__ void __launch_bounds__(kGT) k_c128_to_c64(const double2* in, float2* out, long long n) {
+    for (long long i = blockIdx.x * (long long)kGT + threadIdx.x; i < n; i += (long long)gridDim.x * kGT)
+        out[i] = make_float2((float)in[i].x, (float)in[i].y);
+}
+__global__ void __launch_bounds__(kGT) k_phase(const double2* A, float* phase, long long n) {
+    for (long long i = blockIdx.x * (long long)kGT + threadIdx.x; i < n; i += (long long)gridDim.x * kGT)
+        phase[i] = (float)atan2(A[i].y, A[i].x);
+}
+__global__ void __launch_bounds__(kGT) k_phase_exp(const float* phase, double2* B, long long n) {
+    for (long long i = blockIdx.x * (long long)kGT + threadIdx.x; i < n; i += (long long)gridDim.x * kGT) {
+        double s, c;
+        sincos((double)phase[i], &s, &c);
+        B[i] = make_double2(c, s);
+    }
+}
+__global__ void __launch_bounds__(kGT) k_abs2(const double2* C, float* out, long long n) {
+    for (long long i = blockIdx.x * (long long)kGT + threadIdx.x; i < n; i += (long long)gridDim.x * kGT)
+        out[i] = (float)(C[i].x * C[i].x + C[i].y * C[i].y);
+}
+
+// Statistics block `blockIdx.x` of hologram `blockIdx.y`: a contiguous chunk.
+struct ChunkOf {
+    long long lo, hi;
+    __device__ ChunkOf(long long holo, int nwg) {
+        const long long chunk = (holo + nwg - 1) / nwg;
+        lo = (long long)blockIdx.x * chunk;
+        hi = lo + chunk < holo ? lo + chunk : holo;
+    }
+};
+__device__ __forceinline__ void store_partials(double* partials, int b, int iter, int max_loops, int nwg, double mx,
+                                               double s2, double st) {
+    block_reduce_stats<kGT>(mx, s2, st);
+    if (threadIdx.x == 0) {
+        double* dst = partials + (((long long)b * max_loops + iter) * nwg + blockIdx.x) * 4;
+        dst[0] = mx;
+        dst[1] = s2;
+        dst[2] = st;
+        dst[3] = 0.0;
+    }
+}
+
+// GS: E = |C|^2 and its statistics, expected output, D = a_T C/|C| (src/algorithms.py:33,36-38).
+// A hologram whose checked run has stopped keeps D (and E): its later products repeat.
+__global__ void __launch_bounds__(kGT) k_gs_project(const double2* C, const void* tgt, int tt, double2* D,
+                                                    float* e_out, double* partials, const int* stop, int iter,
+                                                    int checked, int write_e, long long holo, int nwg, int max_loops) {
+    const int b = blockIdx.y;
+    if (checked && iter > stop[b]) return;
+    const ChunkOf ch(holo, nwg);
+    double mx = 0.0, s2 = 0.0, st = 0.0;
+    for (long long r = ch.lo + threadIdx.x; r < ch.hi; r += kGT) {
+        const long long i = (long long)b * holo + r;
+        const double2 z = C[i];
+        const double e = z.x * z.x + z.y * z.y;
+        mx = fmax(mx, e);
+        s2 += e * e;
+        st += e * g_t(tgt, tt, i);
+        if (write_e) e_out[i] = (float)e;
+        D[i] = g_unit(z, g_amp(tgt, tt, i));
+    }
+    store_partials(partials, b, iter, max_loops, nwg, mx, s2, st);
+}
+
+// GD: u = x / |x| a_in (src/algorithms.py:84; |x| = 0 gives NaN as there)
+__global__ void __launch_bounds__(kGT) k_gd_u(const double2* X, double2* U, const float* ain, long long holo,
+                                              long long n) {
+    for (long long i = blockIdx.x * (long long)kGT + threadIdx.x; i < n; i += (long long)gridDim.x * kGT) {
+        const double2 x = X[i];
+        const double r = g_ain(ain, i, holo) / sqrt(x.x * x.x + x.y * x.y);
+        U[i] = make_double2(x.x * r, x.y * r);
+    }
+}
+// GD: P = |F|^2 statistics (max for the normalisation, src/algorithms.py:85-86) and output
+__global__ void __launch_bounds__(kGT) k_gd_stats(const double2* F, const void* tgt, int tt, float* e_out,
+                                                  double* partials, const int* stop, int iter, int checked, int write_e,
+                                                  long long holo, int nwg, int max_loops) {
+    const int b = blockIdx.y;
+    if (checked && iter > stop[b]) return;
+    const ChunkOf ch(holo, nwg);
+    double mx = 0.0, s2 = 0.0, st = 0.0;
+    for (long long r = ch.lo + threadIdx.x; r < ch.hi; r += kGT) {
+        const long long i = (long long)b * holo + r;
+        const double2 z = F[i];
+        const double e = z.x * z.x + z.y * z.y;
+        mx = fmax(mx, e);
+        s2 += e * e;
+        st += e * g_t(tgt, tt, i);
+        if (write_e) e_out[i] = (float)e;
+    }
+    store_partials(partials, b, iter, max_loops, nwg, mx, s2, st);
+}
+// one (hologram, iteration) slab -> stats, and the tolerance test (src/algorithms.py:29,83,92)
+__global__ void __launch_bounds__(256) k_reduce_iter(StatsParams p) {
+    const int b = blockIdx.x;
+    if (p.iter > p.stop_iter[b]) return;
+    __shared__ double o[4];
+    reduce_slab(p, b, p.iter, o);
+    if (threadIdx.x == 0) {
+        for (int k = 0; k < 4; ++k) p.stats[((long long)b * p.max_loops + p.iter) * 4 + k] = o[k];
+        if (p.tol >= 0.0 && !(o[3] > p.tol)) p.stop_iter[b] = p.iter;
+    }
+}
+// GD: G = mask F (s P - T), s = norm / max P, mask = 1 + wa T / 255 (src/algorithms.py:80,85-88)
+__global__ void __launch_bounds__(kGT) k_gd_grad(const double2* F, const void* tgt, int tt, const double* stats,
+                                                 const double* norm, double2* G, float wa, const int* stop, int iter,
+                                                 int checked, long long holo, int max_loops, long long n) {
+    for (long long i = blockIdx.x * (long long)kGT + threadIdx.x; i < n; i += (long long)gridDim.x * kGT) {
+        const int b = (int)(i / holo);
+        if (checked && iter > stop[b]) continue;
+        const double s = norm[b] / stats[((long long)b * max_loops + iter) * 4];
+        const double2 z = F[i];
+        const double t = g_t(tgt, tt, i);
+        // numpy's mask dtype: float32 for a float32 target (the python float scalars are
+        // weak), float64 for uint8 (src/algorithms.py:80)
+        const double mask = tt == TGT_U8 ? 1.0 + (double)wa * t / 255.0
+                                         : (double)(1.0f + __fdiv_rn(__fmul_rn(wa, (float)t), 255.0f));
+        const double w = mask * ((z.x * z.x + z.y * z.y) * s - t);
+        G[i] = make_double2(z.x * w, z.y * w);
+    }
+}
+// GD: dEdF = ifft2(G) a_in, dEdX_complex (src/algorithms.py:179-185), x -= lr dEdX (:91)
+__global__ void __launch_bounds__(kGT) k_gd_update(double2* X, const double2* g, const float* ain, const float* lr,
+                                                   const int* stop, int iter, int checked, double inv_s,
+                                                   long long holo, long long n) {
+    const double l = (double)lr[iter];
+    for (long long i = blockIdx.x * (long long)kGT + threadIdx.x; i < n; i += (long long)gridDim.x * kGT) {
+        const int b = (int)(i / holo);
+        if (checked && iter > stop[b]) continue;
+        const double a = g_ain(ain, i, holo) * inv_s;
+        const double gx = g[i].x * a, gy = g[i].y * a;
+        double2 x = X[i];
+        const double ax2 = x.x * x.x + x.y * x.y;
+        const double ax = sqrt(ax2);
+        const double re = x.x * gx + x.y * gy;
+        x.x -= l * ((gx - x.x * (re / ax2)) / ax);
+        x.y -= l * ((gy - x.y * (re / ax2)) / ax);
+        X[i] = x;
+    }
+}
+
+std::vector<double> dft_matrix(int n) {
+    std::vector<double> m((size_t)n * n * 2);
+    for (long long j = 0; j < n; ++j)
+        for (long long k = 0; k < n; ++k) {
+            const double ang = -2.0 * M_PI * (double)((j * k) % n) / (double)n;
+            m[(j * n + k) * 2] = std::cos(ang);
+            m[(j * n + k) * 2 + 1] = std::sin(ang);
+        }
+    return m;
+}
+
+// out = op2(in): forward (F) or inverse (conj F, unscaled) 2-D transform of
+// [B][H][W] complex128; in may equal out (the product goes through tmp)
+int dft2(GenericEngine* g, const GenericView& v, const double2* in, double2* out, bool inverse) {
+    const rocblas_operation opf = inverse ? rocblas_operation_conjugate_transpose : rocblas_operation_none;
+    const rocblas_double_complex one{1.0, 0.0}, zero{0.0, 0.0};
+    auto cz = [](const double2* p) { return reinterpret_cast<const rocblas_double_complex*>(p); };
+    auto z = [](double2* p) { return reinterpret_cast<rocblas_double_complex*>(p); };
+    G_BLAS(rocblas_zgemm_strided_batched(g->blas, opf, rocblas_operation_none, v.W, v.H, v.W, &one, cz(g->fw), v.W, 0,
+                                         cz(in), v.W, v.holo, &zero, z(g->tmp), v.W, v.holo, v.B));
+    G_BLAS(rocblas_zgemm_strided_batched(g->blas, rocblas_operation_none, opf, v.W, v.H, v.H, &one, cz(g->tmp), v.W,
+                                         v.holo, cz(g->fh), v.H, 0, &zero, z(out), v.W, v.holo, v.B));
+    return 0;
+}
+
+StatsParams stats_of(const GenericView& v, double tol, int iter) {
+    StatsParams s{};
+    s.partials = v.partials;
+    s.stats = v.stats;
+    s.stop_iter = v.stop;
+    s.norm = v.norm;
+    s.sum_t2 = v.sum_t2;
+    s.inv_s = 1.0 / (double)v.holo;
+    s.tol = tol;
+    s.max_loops = v.max_loops;
+    s.nwg = v.nwg;
+    s.iter = iter;
+    return s;
+}
+
+}  // namespace
+
+int generic_nwg(long long holo) { return (int)std::max<long long>(1, std::min<long long>(1024, holo / (kGT * 8))); }
+
+void generic_destroy(GenericEngine* g) {
+    if (!g) return;
+    for (void* p : {(void*)g->a, (void*)g->b, (void*)g->d, (void*)g->x, (void*)g->tmp, (void*)g->fw})
+        if (p) (void)hipFree(p);
+    if (g->fh && g->fh != g->fw) (void)hipFree(g->fh);
+    if (g->blas) (void)rocblas_destroy_handle(g->blas);
+    delete g;
+}
+
+int generic_create(const GenericView& v, GenericEngine** out) {
+    *out = nullptr;
+    GenericEngine* g = new GenericEngine();
+    auto fail_free = [&](int rc) {
+        generic_destroy(g);
+        return rc;
+    };
+    const size_t n = (size_t)v.B * v.holo;
+    auto alloc = [&](double2** p, size_t count) {
+        return hipMalloc((void**)p, count * sizeof(double2)) == hipSuccess;
+    };
+    if (!alloc(&g->a, n) || !alloc(&g->b, n) || !alloc(&g->d, n) || !alloc(&g->tmp, n) ||
+        (v.algo == SLM_ALGO_GD && !alloc(&g->x, n)) || !alloc(&g->fw, (size_t)v.W * v.W))
+        return fail_free(slm_set_error(SLM_ERR_HIP, "DFT engine: device allocation failed"));
+    {
+        const std::vector<double> m = dft_matrix(v.W);
+        if (hipMemcpyAsync(g->fw, m.data(), m.size() * sizeof(double), hipMemcpyHostToDevice, v.stream) !=
+                hipSuccess ||
+            hipStreamSynchronize(v.stream) != hipSuccess)
+            return fail_free(slm_set_error(SLM_ERR_HIP, "DFT engine: matrix upload failed"));
+    }
+    if (v.H == v.W) {
+        g->fh = g->fw;
+    } else {
+        if (!alloc(&g->fh, (size_t)v.H * v.H)) return fail_free(slm_set_error(SLM_ERR_HIP, "DFT engine: allocation"));
+        const std::vector<double> m = dft_matrix(v.H);
+        if (hipMemcpyAsync(g->fh, m.data(), m.size() * sizeof(double), hipMemcpyHostToDevice, v.stream) !=
+                hipSuccess ||
+            hipStreamSynchronize(v.stream) != hipSuccess)
+            return fail_free(slm_set_error(SLM_ERR_HIP, "DFT engine: matrix upload failed"));
+    }
+    if (rocblas_create_handle(&g->blas) != rocblas_status_success ||
+        rocblas_set_stream(g->blas, v.stream) != rocblas_status_success ||
+        rocblas_set_atomics_mode(g->blas, rocblas_atomics_not_allowed) != rocblas_status_success)
+        return fail_free(slm_set_error(SLM_ERR_HIP, "DFT engine: rocBLAS handle setup failed"));
+    *out = g;
+    return 0;
+}
+
+int generic_enqueue(GenericEngine* g, const GenericView& v, int loops, double tol, int checked, float wa,
+                    bool phase_set, bool field_set) {
+    const long long n = (long long)v.B * v.holo;
+    const int grid = grid_of(n);
+    const dim3 sgrid(v.nwg, v.B);
+    hipStream_t st = v.stream;
+    const double tol_or_none = checked ? tol : -1.0;  // k_reduce_iter sets stop flags for checked runs only
+    if (v.algo == SLM_ALGO_GS) {
+        if (phase_set) {
+            hipLaunchKernelGGL(k_warm, dim3(grid), dim3(kGT), 0, st, v.phase_in, g->b, v.ain, v.holo, n);
+        } else {
+            hipLaunchKernelGGL(k_amp, dim3(grid), dim3(kGT), 0, st, v.tgt, v.tt, g->d, n);
+            if (int rc = dft2(g, v, g->d, g->a, true)) return rc;
+            hipLaunchKernelGGL(k_round_c64, dim3(grid), dim3(kGT), 0, st, g->a, n);
+        }
+        for (int i = 0; i < loops; ++i) {
+            if (i > 0 || !phase_set) hipLaunchKernelGGL(k_unit, dim3(grid), dim3(kGT), 0, st, g->a, g->b, v.ain, v.holo, n);
+            if (int rc = dft2(g, v, g->b, g->b, false)) return rc;  // C
+            hipLaunchKernelGGL(k_gs_project, sgrid, dim3(kGT), 0, st, g->b, v.tgt, v.tt, g->d, v.e_out, v.partials,
+                               v.stop, i, checked, (checked || i + 1 == loops) ? 1 : 0, v.holo, v.nwg, v.max_loops);
+            if (int rc = dft2(g, v, g->d, g->a, true)) return rc;  // A = ifft2(D) * S
+            if (checked)
+                hipLaunchKernelGGL(k_reduce_iter, dim3(v.B), dim3(256), 0, st, stats_of(v, tol_or_none, i));
+        }
+        hipLaunchKernelGGL(k_phase, dim3(grid), dim3(kGT), 0, st, g->a, v.phase_out, n);
+    } else {
+        if (field_set) {
+            hipLaunchKernelGGL(k_c64_to_c128, dim3(grid), dim3(kGT), 0, st, v.field0, g->x, n);
+        } else {
+            hipLaunchKernelGGL(k_amp, dim3(grid), dim3(kGT), 0, st, v.tgt, v.tt, g->d, n);
+            if (int rc = dft2(g, v, g->d, g->a, true)) return rc;
+            hipLaunchKernelGGL(k_round_c64, dim3(grid), dim3(kGT), 0, st, g->a, n);
+            hipLaunchKernelGGL(k_fourier, dim3(grid), dim3(kGT), 0, st, g->a, g->x, v.ain, v.holo, n);
+        }
+        const double inv_s = 1.0 / (double)v.holo;
+        for (int i = 0; i < loops; ++i) {
+            hipLaunchKernelGGL(k_gd_u, dim3(grid), dim3(kGT), 0, st, g->x, g->b, v.ain, v.holo, n);
+            if (int rc = dft2(g, v, g->b, g->b, false)) return rc;  // F
+            hipLaunchKernelGGL(k_gd_stats, sgrid, dim3(kGT), 0, st, g->b, v.tgt, v.tt, v.e_out, v.partials, v.stop, i,
+                               checked, (checked || i + 1 == loops) ? 1 : 0, v.holo, v.nwg, v.max_loops);
+            // this iteration's max |F|^2 (and, checked, its error against the tolerance)
+            hipLaunchKernelGGL(k_reduce_iter, dim3(v.B), dim3(256), 0, st, stats_of(v, tol_or_none, i));
+            hipLaunchKernelGGL(k_gd_grad, dim3(grid), dim3(kGT), 0, st, g->b, v.tgt, v.tt, v.stats, v.norm, g->d, wa,
+                               v.stop, i, checked, v.holo, v.max_loops, n);
+            if (int rc = dft2(g, v, g->d, g->a, true)) return rc;  // g = ifft2(G) * S
+            hipLaunchKernelGGL(k_gd_update, dim3(grid), dim3(kGT), 0, st, g->x, g->a, v.ain, v.lr, v.stop, i, checked,
+                               inv_s, v.holo, n);
+        }
+        hipLaunchKernelGGL(k_phase, dim3(grid), dim3(kGT), 0, st, g->x, v.phase_out, n);
+    }
+    G_HIP(hipGetLastError());
+    return 0;
+}
+
+int generic_field(GenericEngine* g, const GenericView& v, float2* out) {
+    if (!g->x) return slm_set_error(SLM_ERR_STATE, "the field is the state of GD plans");
+    const long long n = (long long)v.B * v.holo;
+    hipLaunchKernelGGL(k_c128_to_c64, dim3(grid_of(n)), dim3(kGT), 0, v.stream, g->x, out, n);
+    G_HIP(hipGetLastError());
+    return 0;
+}
+
+int generic_fft2(GenericEngine* g, const GenericView& v, const float2* in, float2* out, int inverse) {
+    const long long n = (long long)v.B * v.holo;
+    hipLaunchKernelGGL(k_c64_to_c128, dim3(grid_of(n)), dim3(kGT), 0, v.stream, in, g->b, n);
+    if (int rc = dft2(g, v, g->b, g->b, inverse != 0)) return rc;
+    hipLaunchKernelGGL(k_c128_to_c64, dim3(grid_of(n)), dim3(kGT), 0, v.stream, g->b, out, n);
+    G_HIP(hipGetLastError());
+    return 0;
+}
+
+int generic_intensity(GenericEngine* g, const GenericView& v, const float* phase, float* out) {
+    const long long n = (long long)v.B * v.holo;
+    hipLaunchKernelGGL(k_phase_exp, dim3(grid_of(n)), dim3(kGT), 0, v.stream, phase, g->b, n);
+    if (int rc = dft2(g, v, g->b, g->b, false)) return rc;
+    hipLaunchKernelGGL(k_abs2, dim3(grid_of(n)), dim3(kGT), 0, v.stream, g->b, out, n);
+    G_HIP(hipGetLastError());
+    return 0;
+}
+
+}  // namespace slm

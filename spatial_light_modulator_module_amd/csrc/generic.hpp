@@ -1,0 +1,50 @@
+// Any-size engine of the GS / GD loops: image sides that no radix plan
+// (plans.hpp) covers. The reference takes any (h, w) (src/algorithms.py:20-27;
+// scipy.fft handles every length), so such plans run their 2-D transforms as
+// complex float64 matrix products with the DFT matrices (rocBLAS ZGEMM on the
+// MI355X matrix cores) and the projections / statistics / GD update as
+// element-wise kernels, all state complex128 in HBM, row-major. slm_capi.hip
+// owns the plan's buffers; this engine owns its work buffers, the DFT matrices
+// and the rocBLAS handle.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace slm {
+
+struct GenericEngine;
+
+// the slm_plan buffers the engine reads and writes (row-major [B][H][W])
+struct GenericView {
+    int algo = 0, B = 0, H = 0, W = 0, tt = 0, has_ain = 0, max_loops = 0, nwg = 0;
+    long long holo = 0;
+    hipStream_t stream = nullptr;
+    const void* tgt = nullptr;      // target intensity (uint8 or float32)
+    const float* ain = nullptr;     // incoming amplitude [H][W] or nullptr
+    const float* phase_in = nullptr;  // GS warm start
+    const float2* field0 = nullptr;   // GD initial field (complex64)
+    const float* lr = nullptr;        // GD learning rate per iteration
+    float* phase_out = nullptr;
+    float* e_out = nullptr;           // |C|^2 (GS) / |F|^2 (GD) of the last iteration, float32
+    double* partials = nullptr;       // [B][max_loops][nwg][4]
+    double* stats = nullptr;          // [B][max_loops][4]
+    int* stop = nullptr;              // [B]
+    const double* norm = nullptr;     // max(T) [B]
+    const double* sum_t2 = nullptr;   // sum T^2 [B]
+};
+
+// statistics blocks per hologram (the partials' nwg)
+int generic_nwg(long long holo);
+int generic_create(const GenericView& v, GenericEngine** out);
+void generic_destroy(GenericEngine* g);
+// one full run (setup, loops iterations, phase and expected output, statistics),
+// enqueued on v.stream
+int generic_enqueue(GenericEngine* g, const GenericView& v, int loops, double tol, int checked, float wa,
+                    bool phase_set, bool field_set);
+// the GD field x after the last run, as complex64 [B][H][W] (device)
+int generic_field(GenericEngine* g, const GenericView& v, float2* out);
+// unscaled 2-D DFT of complex64 [B][H][W] (device in / out; in may equal out)
+int generic_fft2(GenericEngine* g, const GenericView& v, const float2* in, float2* out, int inverse);
+// |fft2(exp(i phase))|^2, float32 [B][H][W] (device)
+int generic_intensity(GenericEngine* g, const GenericView& v, const float* phase, float* out);
+
+}  // namespace slm

@@ -23,6 +23,7 @@
 
 #include "../../include/slm_hip.h"
 #include "dispatch.hpp"
+#include "generic.hpp"
 #define SLM_DEFINE_SMALL_KERNELS
 #include "kernels.hpp"
 
@@ -351,6 +352,9 @@ struct slm_plan {
     // and relaunched as one graph -- 3 % per 1024^2 GS iteration, 6 % at 256^2
     // (gpurun_out/exp17: the inter-kernel gaps of 400 dependent launches)
     hipEvent_t marks[2] = {nullptr, nullptr};  // slm_plan_mark stopwatch
+    // sides without a radix plan: the DFT-GEMM engine (generic.hpp) runs the
+    // loop; state and arrays row-major, float64 arithmetic
+    GenericEngine* gen = nullptr;
     hipGraphExec_t gexec = nullptr;
     int g_loops = -1, g_checked = -1, g_state = -1;
     double g_tol = 0.0;
@@ -800,6 +804,33 @@ int recover_grid_fault(slm_plan* p, bool* faulted) {
     return 0;
 }
 
+GenericView gview(slm_plan* p) {
+    GenericView v;
+    v.algo = p->algo;
+    v.B = p->B;
+    v.H = p->H;
+    v.W = p->W;
+    v.tt = p->tt;
+    v.has_ain = p->has_ain;
+    v.max_loops = p->max_loops;
+    v.nwg = p->nwg;
+    v.holo = p->holo;
+    v.stream = p->stream;
+    v.tgt = p->tgt;
+    v.ain = p->ain;
+    v.phase_in = p->phase_in;
+    v.field0 = p->field0;
+    v.lr = p->lr;
+    v.phase_out = p->phase_out;
+    v.e_out = p->e_out;
+    v.partials = p->partials;
+    v.stats = p->stats;
+    v.stop = p->stop;
+    v.norm = p->norm;
+    v.sum_t2 = p->sum_t2;
+    return v;
+}
+
 int enqueue_run(slm_plan* p, int loops, double tol, int checked, float wa) {
     if (!p) return fail(SLM_ERR_ARG, "null plan");
     if (!p->target_set) return fail(SLM_ERR_STATE, "target not set");
@@ -810,7 +841,10 @@ int enqueue_run(slm_plan* p, int loops, double tol, int checked, float wa) {
     p->field_fresh = false;  // the run writes the field
     RC(launch(p, SLM_KERNEL_OTHER, fill_int_kernel, dim3((p->B + 255) / 256), dim3(256), p->stop, p->B,
               (int)INT_MAX));
-    RC(p->algo == SLM_ALGO_GS ? enqueue_gs(p, loops, tol, checked) : enqueue_gd(p, loops, tol, checked, wa));
+    if (p->gen)
+        RC(generic_enqueue(p->gen, gview(p), loops, tol, checked, wa, p->phase_set, p->field_set));
+    else
+        RC(p->algo == SLM_ALGO_GS ? enqueue_gs(p, loops, tol, checked) : enqueue_gd(p, loops, tol, checked, wa));
     StatsParams s = stats_params(p, tol);
     RC(launch(p, SLM_KERNEL_OTHER, stats_reduce_kernel, dim3(loops, p->B), dim3(256), s));
     return 0;
@@ -834,6 +868,7 @@ void free_plan(slm_plan* p) {
         (void)hipEventDestroy(e.second);
     }
     if (p->gexec) (void)hipGraphExecDestroy(p->gexec);
+    generic_destroy(p->gen);
     for (hipEvent_t e : p->marks)
         if (e) (void)hipEventDestroy(e);
     if (p->stream) (void)hipStreamDestroy(p->stream);
@@ -942,11 +977,9 @@ int plan_create_on(int device, int algo, int batch, int height, int width, int t
     if (algo != SLM_ALGO_GS && algo != SLM_ALGO_GD) return fail(SLM_ERR_ARG, "unknown algorithm %d", algo);
     if (batch < 1 || max_loops < 1) return fail(SLM_ERR_ARG, "batch and max_loops must be >= 1");
     if (tgt_type != SLM_TGT_U8 && tgt_type != SLM_TGT_F32) return fail(SLM_ERR_ARG, "unknown target type");
-    if (!slm_supported_length(height) || !slm_supported_length(width))
-        return fail(SLM_ERR_UNSUPPORTED,
-                    "image shape %dx%d unsupported: each side must be one of 64, 128, 256, 512, 768, 1024, "
-                    "2048, 4096",
-                    height, width);
+    if (height < 1 || width < 1) return fail(SLM_ERR_ARG, "image shape %dx%d", height, width);
+    // sides without a radix plan (plans.hpp) run the DFT-GEMM engine (generic.hpp)
+    const bool generic = !slm_supported_length(height) || !slm_supported_length(width);
     HIP_TRY(hipSetDevice(device));
     slm_plan* p = new slm_plan();
     p->algo = algo;
@@ -975,19 +1008,28 @@ int plan_create_on(int device, int algo, int batch, int height, int width, int t
     if (const char* e = std::getenv("SLM_PRECISION")) p->prec = (std::strcmp(e, "f64") == 0) ? PREC_F64 : PREC_F32;
     // buffers indexed by column panel / row group hold the finer tiling of both precisions
     int max_nwg = 0, min_rpw = INT_MAX;
-    const int want = p->prec;
-    for (int prec : {PREC_F32, PREC_F64}) {
-        int rc = configure(p, prec);
-        if (rc) {
+    if (generic) {
+        p->dev_tt = tgt_type;  // row-major target, amplitude formed where used
+        p->prec = PREC_F64;
+        p->lid = LAYOUT_DEFAULT;
+        p->cw = 0;
+        p->nwg = max_nwg = generic_nwg(p->holo);
+        p->rpw = min_rpw = 1;
+    } else {
+        const int want = p->prec;
+        for (int prec : {PREC_F32, PREC_F64}) {
+            int rc = configure(p, prec);
+            if (rc) {
+                delete p;
+                return rc;
+            }
+            max_nwg = std::max(max_nwg, p->nwg);
+            min_rpw = std::min(min_rpw, p->rpw);
+        }
+        if (int rc = configure(p, want)) {
             delete p;
             return rc;
         }
-        max_nwg = std::max(max_nwg, p->nwg);
-        min_rpw = std::min(min_rpw, p->rpw);
-    }
-    if (int rc = configure(p, want)) {
-        delete p;
-        return rc;
     }
     const size_t n = (size_t)batch * p->holo;
     const size_t tb = tgt_type == SLM_TGT_U8 ? 1 : 4;
@@ -1004,9 +1046,12 @@ int plan_create_on(int device, int algo, int batch, int height, int width, int t
         delete p;
         return fail(SLM_ERR_HIP, "stream creation failed: %s", hipGetErrorString(se));
     }
-    RC(alloc((void**)&p->xa, n * sizeof(float2)));
-    RC(alloc((void**)&p->y, n * sizeof(float2)));
-    if (algo == SLM_ALGO_GD) {
+    RC(alloc((void**)&p->xa, n * sizeof(float2)));  // generic plans: complex64 staging (fft2, read_field)
+    if (!generic) RC(alloc((void**)&p->y, n * sizeof(float2)));
+    if (algo == SLM_ALGO_GD && generic) {
+        RC(alloc((void**)&p->field0, n * sizeof(float2)));
+        RC(alloc((void**)&p->lr, (size_t)max_loops * sizeof(float)));
+    } else if (algo == SLM_ALGO_GD) {
         RC(alloc((void**)&p->xb, n * sizeof(float2)));
         RC(alloc((void**)&p->field, n * sizeof(float2)));
         RC(alloc((void**)&p->field0, n * sizeof(float2)));
@@ -1035,9 +1080,15 @@ int plan_create_on(int device, int algo, int batch, int height, int width, int t
     RC(alloc((void**)&p->normf, (size_t)batch * sizeof(float)));
     RC(alloc((void**)&p->sum_t2, (size_t)batch * sizeof(double)));
     RC(alloc((void**)&p->ts_part, (size_t)batch * ts_blocks(p->holo) * 2 * sizeof(double)));
-    if (const char* e = std::getenv("SLM_TRACE_BUF"); e && std::atoi(e)) {
+    if (const char* e = std::getenv("SLM_TRACE_BUF"); e && std::atoi(e) && !generic) {
         RC(alloc((void**)&p->trace_col, (size_t)batch * max_nwg * kTraceSlots * sizeof(unsigned long long)));
         RC(alloc((void**)&p->trace_row, (size_t)batch * (height / min_rpw) * kTraceSlots * sizeof(unsigned long long)));
+    }
+    if (generic) {
+        if (int rc = generic_create(gview(p), &p->gen)) {
+            free_plan(p);
+            return rc;
+        }
     }
     *out = p;
     return 0;
@@ -1068,13 +1119,20 @@ int slm_plan_set_target(slm_plan* p, const void* tgt) {
     HIP_TRY(hipSetDevice(p->device));
     const long long n = (long long)p->B * p->holo;
     const size_t tb = p->tt == SLM_TGT_U8 ? 1 : 4;
-    void* stage = p->e_out;  // n floats >= n target elements of either type
+    void* stage = p->gen ? p->tgt : p->e_out;  // generic plans keep the row-major target as uploaded
     // host arrays stay pageable: HIP's staged copies run at ~45 GB/s for a 4 MB
     // target here; pinning the caller's buffer or a pinned staging buffer plus a
     // host memcpy measured no faster (tools/xfer_probe.py)
     HIP_TRY(hipMemcpyAsync(stage, tgt, (size_t)n * tb, hipMemcpyHostToDevice, p->stream));
     const int nblk = ts_blocks(p->holo);
-    if (p->tt == SLM_TGT_U8) {
+    if (p->gen) {
+        if (p->tt == SLM_TGT_U8)
+            hipLaunchKernelGGL(target_stats_partial_kernel<uint8_t>, dim3(nblk, p->B), dim3(kTsThreads), 0,
+                               p->stream, (const uint8_t*)stage, p->holo, p->ts_part);
+        else
+            hipLaunchKernelGGL(target_stats_partial_kernel<float>, dim3(nblk, p->B), dim3(kTsThreads), 0,
+                               p->stream, (const float*)stage, p->holo, p->ts_part);
+    } else if (p->tt == SLM_TGT_U8) {
         hipLaunchKernelGGL(target_stats_partial_kernel<uint8_t>, dim3(nblk, p->B), dim3(kTsThreads), 0, p->stream,
                            (const uint8_t*)stage, p->holo, p->ts_part);
         RC(relayout(layout_x_log2(p->lid), (const uint8_t*)stage, (uint8_t*)p->tgt, n, p->H, p->W, true, p->stream));
@@ -1104,6 +1162,7 @@ int slm_plan_set_precision(slm_plan* p, int precision) {
     if (!p) return fail(SLM_ERR_ARG, "null plan");
     if (precision != SLM_PRECISION_F32 && precision != SLM_PRECISION_F64)
         return fail(SLM_ERR_ARG, "unknown precision %d", precision);
+    if (p->gen) return 0;  // the DFT-GEMM engine computes in float64 only
     HIP_TRY(hipSetDevice(p->device));
     RC(configure(p, precision));
     return 0;
@@ -1148,8 +1207,12 @@ int slm_plan_set_field(slm_plan* p, const float* field) {
         return 0;
     }
     const long long n = (long long)p->B * p->holo;
-    HIP_TRY(hipMemcpyAsync(p->y, field, (size_t)n * sizeof(float2), hipMemcpyHostToDevice, p->stream));
-    RC(relayout(layout_y_log2(p->lid), (const float2*)p->y, p->field0, n, p->H, p->W, true, p->stream));
+    if (p->gen) {
+        HIP_TRY(hipMemcpyAsync(p->field0, field, (size_t)n * sizeof(float2), hipMemcpyHostToDevice, p->stream));
+    } else {
+        HIP_TRY(hipMemcpyAsync(p->y, field, (size_t)n * sizeof(float2), hipMemcpyHostToDevice, p->stream));
+        RC(relayout(layout_y_log2(p->lid), (const float2*)p->y, p->field0, n, p->H, p->W, true, p->stream));
+    }
     HIP_TRY(hipStreamSynchronize(p->stream));
     p->field_set = true;
     p->field_fresh = true;
@@ -1179,7 +1242,7 @@ int slm_plan_run(slm_plan* p, int loops, double tol, int checked, float wa) {
         const char* e = std::getenv("SLM_GRAPH");
         return !e || std::atoi(e) != 0;
     }();
-    if (!p || !use_graph) return enqueue_run(p, loops, tol, checked, wa);
+    if (!p || !use_graph || p->gen) return enqueue_run(p, loops, tol, checked, wa);  // rocBLAS calls: not captured
     const int state = (p->phase_set ? 1 : 0) | (p->field_set ? 2 : 0);
     if (!p->gexec || p->g_state != state || p->g_loops != loops || p->g_tol != tol || p->g_checked != checked || p->g_wa != wa) {
         HIP_TRY(hipSetDevice(p->device));
@@ -1324,6 +1387,7 @@ int slm_plan_set_target_stats(slm_plan* p, const double* norm, const double* sum
 
 long long slm_plan_kernel_bytes(slm_plan* p, int cls) {
     if (!p) return -1;
+    if (p->gen) return 0;  // the DFT-GEMM engine has no column / row kernel classes
     const long long px = (long long)p->B * p->holo;
     const long long tb = p->tt == SLM_TGT_U8 ? 1 : 4;
     const long long ab = p->has_ain ? 4 : 0;
@@ -1353,6 +1417,10 @@ int slm_plan_info(slm_plan* p, int* info) {
 int slm_plan_engine(slm_plan* p, int* col_engine, int* row_engine) {
     if (!p || !col_engine || !row_engine) return fail(SLM_ERR_ARG, "null argument");
     // mirrors kernels.hpp: kShuffle<K, P> && (CW == 2 | RPW == 2) && one line per thread
+    if (p->gen) {
+        *col_engine = *row_engine = 2;  // DFT-GEMM (generic.hpp)
+        return 0;
+    }
     auto shuf = [&](int key) {
         return SLM_SHUFFLE && p->prec == PREC_F32 && key >= 0 && kPlans[key].n == kShufN && kPlans[key].e == 8;
     };
@@ -1365,6 +1433,10 @@ int slm_plan_device(slm_plan* p) { return p ? p->device : -1; }
 
 int slm_plan_layout(slm_plan* p, int* x_log2, int* y_log2) {
     if (!p || !x_log2 || !y_log2) return fail(SLM_ERR_ARG, "null argument");
+    if (p->gen) {
+        *x_log2 = *y_log2 = 0;  // row-major
+        return 0;
+    }
     *x_log2 = layout_x_log2(p->lid);
     *y_log2 = layout_y_log2(p->lid);
     return 0;
@@ -1490,6 +1562,14 @@ int slm_fft2(const float* in, float* out, int batch, int height, int width, int 
     const long long n = (long long)batch * p->holo;
     const size_t bytes = (size_t)n * sizeof(float2);
     int rc = 0;
+    if (p->gen) {  // DFT-GEMM engine: row-major in place through the staging buffer
+        hipError_t e = hipMemcpyAsync(p->xa, in, bytes, hipMemcpyHostToDevice, p->stream);
+        if (e != hipSuccess) rc = fail(SLM_ERR_HIP, "upload failed: %s", hipGetErrorString(e));
+        if (!rc) rc = generic_fft2(p->gen, gview(p), p->xa, p->xa, inverse);
+        if (!rc) rc = copy_sync(out, p->xa, bytes, hipMemcpyDeviceToHost, p->stream);
+        free_plan(p);
+        return rc;
+    }
     hipError_t e = hipMemcpyAsync(p->y, in, bytes, hipMemcpyHostToDevice, p->stream);
     if (e != hipSuccess) rc = fail(SLM_ERR_HIP, "upload failed: %s", hipGetErrorString(e));
     if (!rc) rc = relayout(layout_y_log2(p->lid), (const float2*)p->y, p->xa, n, height, width, true, p->stream);  // row-pass input
@@ -1521,7 +1601,9 @@ int slm_fft2_intensity(const float* phase, int batch, int height, int width, flo
     slm_plan* p = nullptr;
     RC(slm_plan_create(SLM_ALGO_GS, batch, height, width, SLM_TGT_F32, 0, 1, &p));
     int rc = slm_plan_set_phase(p, phase);
-    if (!rc) {
+    if (!rc && p->gen) {
+        rc = generic_intensity(p->gen, gview(p), p->phase_in, p->e_out);
+    } else if (!rc) {
         // fft2(exp(1j phase)) = column FFT of the row-transformed field; |.|^2 row-major
         RowParams rp = row_params(p);
         rp.out = p->xa;
@@ -1544,6 +1626,15 @@ int slm_plan_read_field(slm_plan* p, float* field) {
     if (p->algo != SLM_ALGO_GD) return fail(SLM_ERR_STATE, "the field is the state of GD plans");
     HIP_TRY(hipSetDevice(p->device));
     const long long n = (long long)p->B * p->holo;
+    if (p->gen) {
+        const float2* src = p->field0;
+        if (!p->field_fresh) {
+            RC(generic_field(p->gen, gview(p), p->xa));
+            src = p->xa;
+        }
+        RC(copy_sync(field, src, (size_t)n * sizeof(float2), hipMemcpyDeviceToHost, p->stream));
+        return 0;
+    }
     // p->y is scratch between runs (every run rewrites it before reading it); a
     // field set since the last run is read back from field0 (runs never write it)
     const float2* src = p->field_fresh ? p->field0 : p->field;

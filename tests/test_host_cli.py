@@ -128,9 +128,13 @@ def test_gd_argument_errors():
         alg.gradient_descent(t, _args(max_loops=1, unsettle=5))
 
 
-def test_unsupported_shape_is_rejected():
+def test_shape_checks():
+    """Any (h, w) is accepted, as the reference's (src/algorithms.py:20-27);
+    only a non-2-D target fails the reference's own unpacking."""
+    assert alg._check_shape(np.ones((100, 64))) == (100, 64)
+    assert alg._check_shape(np.ones((1, 3))) == (1, 3)
     with pytest.raises(ValueError):
-        alg.gerchberg_saxton(np.ones((100, 64)), _args())
+        alg.gerchberg_saxton(np.ones((4, 100, 64)), _args())
 
 
 @pytest.mark.parametrize("loops,unsettle", [(10, 0), (10, 1), (12, 3), (7, 2), (100, 4)])

@@ -24,5 +24,5 @@ done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=fast -fno-slp-vectorize -Wno-unused-function $extra -I/opt/rocm/include -c $src/slm_capi.hip -o $out/slm_capi.o &
 pids="$pids $!"
 for p in $pids; do wait $p; done
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $root/spatial_light_modulator_module_amd/lib/libslm_hip_$name.so $objs $out/slm_capi.o $base/frames.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $root/spatial_light_modulator_module_amd/lib/libslm_hip_$name.so $objs $out/slm_capi.o $base/frames.o $base/generic.o -L/opt/rocm/lib -lrccl -lrocblas -Wl,-rpath,/opt/rocm/lib
 echo built libslm_hip_$name.so

@@ -14,5 +14,5 @@ for f in $base/kernels_*.o; do
   if [[ " $* " == *" $k "* ]]; then objs="$objs $out/kernels_$k.o"; else objs="$objs $f"; fi
 done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=fast -fno-slp-vectorize -Wno-unused-function $extra -I/opt/rocm/include -c $src/slm_capi.hip -o $out/slm_capi.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $root/spatial_light_modulator_module_amd/lib/libslm_hip_$name.so $objs $out/slm_capi.o $base/frames.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $root/spatial_light_modulator_module_amd/lib/libslm_hip_$name.so $objs $out/slm_capi.o $base/frames.o $base/generic.o -L/opt/rocm/lib -lrccl -lrocblas -Wl,-rpath,/opt/rocm/lib
 echo relinked libslm_hip_$name.so
