@@ -224,7 +224,7 @@ __device__ __forceinline__ void shuffle_p3(float2 (&v)[8], const ShuffleTw& tw) 
 // D out -- slot m of the thread then holds element (frequency) t + 128 m.
 // Every thread of the workgroup must call it (LDS barrier); lds: 2048 complex64.
 template <bool INV>
-__device__ __forceinline__ void shuffle_first(float2 (&v)[8], int tid, const ShuffleTw& tw, float2* lds) {
+__device__ __forceinline__ void shuffle_first_scalar(float2 (&v)[8], int tid, const ShuffleTw& tw, float2* lds) {
     shuffle_p1<INV, true>(v, tw);
     shuffle_x1(v);
     shuffle_p2<INV, true>(v, tw);
@@ -237,7 +237,7 @@ __device__ __forceinline__ void shuffle_first(float2 (&v)[8], int tid, const Shu
 // state A out. lds: 2048 complex64, not the buffer of the first transform
 // (one barrier per exchange then suffices).
 template <bool INV>
-__device__ __forceinline__ void shuffle_second(float2 (&v)[8], int tid, const ShuffleTw& tw, float2* lds) {
+__device__ __forceinline__ void shuffle_second_scalar(float2 (&v)[8], int tid, const ShuffleTw& tw, float2* lds) {
     Dft<8, INV, float2>::run(v);
     shuffle_x3(v);
     shuffle_p3<INV, false>(v, tw);
@@ -247,8 +247,255 @@ __device__ __forceinline__ void shuffle_second(float2 (&v)[8], int tid, const Sh
     shuffle_p1<INV, false>(v, tw);
 }
 
+// --- packed float32 arithmetic ----------------------------------------------
+// gfx950 executes v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32 on (re, im) pairs
+// at the issue rate of one scalar instruction, with per-half source selects
+// (op_sel) and negations, so a complex add is one instruction instead of two
+// and a complex product two instead of four. The butterflies below are the
+// same DFTs as fft_core.hpp's Dft<4> / Dft<8> (same additions in the same
+// order); products round as fma(x, a, -(y b)) / fma(x, b, y a) (scalar
+// contraction was the compiler's choice per site). Off by default: measured
+// neutral at 1024^2 (column pass 8.62 against 8.57 us, row 7.84 / 7.89 us;
+// the pair is bound by its loads and exchanges, not by VALU issue) with a
+// smaller float32 margin on the 200-iteration gate (6.54e-6 against 5.75e-6),
+// profiles/r04/ab_packed_s5.txt. -DSLM_PACKED=1 builds it (A/B).
+#ifndef SLM_PACKED
+#define SLM_PACKED 0
+#endif
+typedef float pk2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ pk2 to_pk(float2 a) {
+    pk2 r;
+    r.x = a.x;
+    r.y = a.y;
+    return r;
+}
+__device__ __forceinline__ float2 from_pk(pk2 a) { return make_float2(a.x, a.y); }
+__device__ __forceinline__ pk2 pk_fma(pk2 a, pk2 b, pk2 c) { return __builtin_elementwise_fma(a, b, c); }
+// a * w
+__device__ __forceinline__ pk2 pk_mul(pk2 a, pk2 w) {
+    pk2 t = a.yy * w.yx;  // (y wy, y wx)
+    t.x = -t.x;
+    return pk_fma(a.xx, w, t);
+}
+// a * conj(w)
+__device__ __forceinline__ pk2 pk_mulc(pk2 a, pk2 w) {
+    pk2 t = a.yx * w.yy;  // (y wy, x wy)
+    t.y = -t.y;
+    return pk_fma(a, w.xx, t);
+}
+// times the constant exp(-+2 pi i K / R) (fft_core.hpp, twc)
+template <int K, int R, bool INV>
+__device__ __forceinline__ pk2 pk_twc(pk2 a) {
+    constexpr int q = ((48 / R) * K) % 48;
+    if constexpr (q == 0) {
+        return a;
+    } else if constexpr (q == 24) {
+        return -a;
+    } else if constexpr (q == 12 || q == 36) {  // forward q = 12: * (-i); q = 36: * (+i)
+        constexpr bool minus_i = (q == 12) != INV;
+        pk2 r = a.yx;
+        if constexpr (minus_i)
+            r.y = -r.y;  // (y, -x)
+        else
+            r.x = -r.x;  // (-y, x)
+        return r;
+    } else {
+        constexpr float c = (float)cos48(q);
+        constexpr float sn = (float)(INV ? sin48(q) : -sin48(q));
+        pk2 cs;
+        cs.x = c;
+        cs.y = sn;
+        pk2 t = a.yy * cs.yx;  // (y s, y c)
+        t.x = -t.x;
+        return pk_fma(a.xx, cs, t);
+    }
+}
+template <bool INV>
+__device__ __forceinline__ void pk_dft4(pk2* v) {
+    const pk2 a = v[0] + v[2], b = v[0] - v[2], c = v[1] + v[3];
+    const pk2 d = pk_twc<1, 4, INV>(v[1] - v[3]);
+    v[0] = a + c;
+    v[2] = a - c;
+    v[1] = b + d;
+    v[3] = b - d;
+}
+// 8 = 2 x 4 (fft_core.hpp, dft_split<2, 4>)
+template <bool INV>
+__device__ __forceinline__ void pk_dft8(pk2* v) {
+    pk2 z[8];
+    static_for<4>([&](auto n2c) {
+        constexpr int n2 = decltype(n2c)::value;
+        const pk2 a = v[n2], b = v[4 + n2];
+        z[n2 * 2 + 0] = a + b;
+        z[n2 * 2 + 1] = pk_twc<n2, 8, INV>(a - b);
+    });
+    static_for<2>([&](auto k1c) {
+        constexpr int k1 = decltype(k1c)::value;
+        pk2 row[4] = {z[k1], z[2 + k1], z[4 + k1], z[6 + k1]};
+        pk_dft4<INV>(row);
+        static_for<4>([&](auto k2c) {
+            constexpr int k2 = decltype(k2c)::value;
+            v[k1 + 2 * k2] = row[k2];
+        });
+    });
+}
+template <bool INV>
+__device__ __forceinline__ pk2 pk_tw(pk2 a, float2 w) {
+    return INV ? pk_mulc(a, to_pk(w)) : pk_mul(a, to_pk(w));
+}
+__device__ __forceinline__ void pk_swap_l4(pk2& a, pk2& b) {
+    const auto x = __builtin_amdgcn_permlane16_swap(as_u(a.x), as_u(b.x), false, false);
+    const auto y = __builtin_amdgcn_permlane16_swap(as_u(a.y), as_u(b.y), false, false);
+    a.x = as_f(x[0]);
+    a.y = as_f(y[0]);
+    b.x = as_f(x[1]);
+    b.y = as_f(y[1]);
+}
+__device__ __forceinline__ void pk_swap_l5(pk2& a, pk2& b) {
+    const auto x = __builtin_amdgcn_permlane32_swap(as_u(a.x), as_u(b.x), false, false);
+    const auto y = __builtin_amdgcn_permlane32_swap(as_u(a.y), as_u(b.y), false, false);
+    a.x = as_f(x[0]);
+    a.y = as_f(y[0]);
+    b.x = as_f(x[1]);
+    b.y = as_f(y[1]);
+}
+__device__ __forceinline__ void pk_x1(pk2 (&v)[8]) {
+    pk_swap_l4(v[0], v[2]);
+    pk_swap_l4(v[1], v[3]);
+    pk_swap_l4(v[4], v[6]);
+    pk_swap_l4(v[5], v[7]);
+    pk_swap_l5(v[0], v[4]);
+    pk_swap_l5(v[1], v[5]);
+    pk_swap_l5(v[2], v[6]);
+    pk_swap_l5(v[3], v[7]);
+}
+__device__ __forceinline__ void pk_x3(pk2 (&v)[8]) {
+    pk_swap_l4(v[0], v[1]);
+    pk_swap_l4(v[2], v[3]);
+    pk_swap_l4(v[4], v[5]);
+    pk_swap_l4(v[6], v[7]);
+    pk_swap_l5(v[0], v[2]);
+    pk_swap_l5(v[1], v[3]);
+    pk_swap_l5(v[4], v[6]);
+    pk_swap_l5(v[5], v[7]);
+}
+template <bool B_TO_C>
+__device__ __forceinline__ void pk_x2(pk2 (&v)[8], int tid, float2* buf) {
+    const int line = tid & 1;
+    pk2* b = reinterpret_cast<pk2*>(buf);
+    static_for<8>([&](auto mc) {
+        constexpr int m = decltype(mc)::value;
+        b[shuffle_slot(B_TO_C ? shuffle_pos_b(tid, m) : shuffle_pos_c(tid, m), line)] = v[m];
+    });
+    lds_barrier();
+    static_for<8>([&](auto mc) {
+        constexpr int m = decltype(mc)::value;
+        v[m] = b[shuffle_slot(B_TO_C ? shuffle_pos_c(tid, m) : shuffle_pos_b(tid, m), line)];
+    });
+}
+template <bool INV, bool DIF, int BASE, int STRIDE>
+__device__ __forceinline__ void pk_r4(pk2 (&v)[8], const float2* w) {
+    pk2 u[4];
+    static_for<4>([&](auto dc) {
+        constexpr int d = decltype(dc)::value;
+        u[d] = v[BASE + STRIDE * d];
+    });
+    if constexpr (!DIF) {
+        static_for<3>([&](auto rc) {
+            constexpr int r = decltype(rc)::value + 1;
+            u[r] = pk_tw<INV>(u[r], w[r - 1]);
+        });
+    }
+    pk_dft4<INV>(u);
+    if constexpr (DIF) {
+        static_for<3>([&](auto rc) {
+            constexpr int r = decltype(rc)::value + 1;
+            u[r] = pk_tw<INV>(u[r], w[r - 1]);
+        });
+    }
+    static_for<4>([&](auto dc) {
+        constexpr int d = decltype(dc)::value;
+        v[BASE + STRIDE * d] = u[d];
+    });
+}
+template <bool INV, bool DIF>
+__device__ __forceinline__ void pk_p1(pk2 (&v)[8], const ShuffleTw& tw) {
+    if constexpr (!DIF) {
+        static_for<7>([&](auto rc) {
+            constexpr int r = decltype(rc)::value + 1;
+            v[r] = pk_tw<INV>(v[r], tw.p1[r - 1]);
+        });
+    }
+    pk_dft8<INV>(v);
+    if constexpr (DIF) {
+        static_for<7>([&](auto rc) {
+            constexpr int r = decltype(rc)::value + 1;
+            v[r] = pk_tw<INV>(v[r], tw.p1[r - 1]);
+        });
+    }
+}
+template <bool INV, bool DIF>
+__device__ __forceinline__ void pk_p2(pk2 (&v)[8], const ShuffleTw& tw) {
+    pk_r4<INV, DIF, 0, 2>(v, tw.p2);
+    pk_r4<INV, DIF, 1, 2>(v, tw.p2);
+}
+template <bool INV, bool DIF>
+__device__ __forceinline__ void pk_p3(pk2 (&v)[8], const ShuffleTw& tw) {
+    pk_r4<INV, DIF, 0, 1>(v, tw.p3);
+    pk_r4<INV, DIF, 4, 1>(v, tw.p3 + 3);
+}
+template <bool INV>
+__device__ __forceinline__ void pk_first(pk2 (&v)[8], int tid, const ShuffleTw& tw, float2* lds) {
+    pk_p1<INV, true>(v, tw);
+    pk_x1(v);
+    pk_p2<INV, true>(v, tw);
+    pk_x2<true>(v, tid, lds);
+    pk_p3<INV, true>(v, tw);
+    pk_x3(v);
+    pk_dft8<INV>(v);
+}
+template <bool INV>
+__device__ __forceinline__ void pk_second(pk2 (&v)[8], int tid, const ShuffleTw& tw, float2* lds) {
+    pk_dft8<INV>(v);
+    pk_x3(v);
+    pk_p3<INV, false>(v, tw);
+    pk_x2<false>(v, tid, lds);
+    pk_p2<INV, false>(v, tw);
+    pk_x1(v);
+    pk_p1<INV, false>(v, tw);
+}
+__device__ __forceinline__ void pk_load(pk2 (&w)[8], const float2 (&v)[8]) {
+    static_for<8>([&](auto mc) { w[decltype(mc)::value] = to_pk(v[decltype(mc)::value]); });
+}
+__device__ __forceinline__ void pk_store(float2 (&v)[8], const pk2 (&w)[8]) {
+    static_for<8>([&](auto mc) { v[decltype(mc)::value] = from_pk(w[decltype(mc)::value]); });
+}
+
 // Transform (INV1), epi(0, m, z) on every output (slot m = element t + 128 m),
 // transform (INV2); v in state A in and out. lds: 2 x 2048 complex64.
+template <bool INV>
+__device__ __forceinline__ void shuffle_first(float2 (&v)[8], int tid, const ShuffleTw& tw, float2* lds) {
+#if SLM_PACKED
+    pk2 w[8];
+    pk_load(w, v);
+    pk_first<INV>(w, tid, tw, lds);
+    pk_store(v, w);
+#else
+    shuffle_first_scalar<INV>(v, tid, tw, lds);
+#endif
+}
+template <bool INV>
+__device__ __forceinline__ void shuffle_second(float2 (&v)[8], int tid, const ShuffleTw& tw, float2* lds) {
+#if SLM_PACKED
+    pk2 w[8];
+    pk_load(w, v);
+    pk_second<INV>(w, tid, tw, lds);
+    pk_store(v, w);
+#else
+    shuffle_second_scalar<INV>(v, tid, tw, lds);
+#endif
+}
+
 template <bool INV1, bool INV2, class Epi>
 __device__ __forceinline__ void shuffle_pair(float2 (&v)[8], int tid, const ShuffleTw& tw, float2* lds, Epi&& epi) {
     shuffle_first<INV1>(v, tid, tw, lds);

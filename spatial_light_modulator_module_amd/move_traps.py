@@ -28,18 +28,25 @@ def _trap_index(black_image: np.ndarray, coords, which):
 
 
 def update_hologram(black_image: np.ndarray, coords, which) -> np.ndarray:
-    """src/move_traps.py:64-68. ``black_image`` must be blank (it always is in
-    the reference's loop, src/move_traps.py:16); the pixel under the trap is
-    left at 0 afterwards, as the reference leaves it."""
+    """src/move_traps.py:64-68: angle(ifft2(image with the trap pixel at 255)),
+    float64; the pixel under the trap is left at 0 afterwards, as the reference
+    leaves it. A blank image (the reference's loop, src/move_traps.py:16) takes
+    the closed form (slm_trap_frames, exact phase index). Any other image runs
+    the device's inverse 2-D transform in complex64 (slm_fft2): the phase is then
+    as accurate as the field's float32 rounding allows (~1e-7 of the field's
+    largest value; tests/test_frames.py)."""
     black_image = np.asarray(black_image)
     if black_image.ndim != 2:
         raise ValueError("black_image must be a 2-D image")
     y, x = _trap_index(black_image, coords, which)
-    if np.count_nonzero(black_image):
-        raise ValueError("update_hologram: black_image must be blank (all zeros) apart from the trap it adds")
-    phase, _ = _lib.trap_frames(black_image.shape, [y], [x], frame=False)
+    if not np.count_nonzero(black_image):
+        phase, _ = _lib.trap_frames(black_image.shape, [y], [x], frame=False)
+        black_image[y][x] = 0
+        return phase[0]
+    black_image[y][x] = 255
+    field = _lib.fft2(black_image.astype(np.complex64), inverse=True)  # unscaled: the 1/(h w) leaves angles alone
     black_image[y][x] = 0
-    return phase[0]
+    return np.angle(field).astype(np.float64)
 
 
 def hologram_frame(hologram: np.ndarray, mask, mask_flag: bool, ct2pi) -> np.ndarray:

@@ -86,6 +86,32 @@ def test_trap_phase_matches_reference(gpu, shape):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(256, 256), (768, 1024), (90, 150)])
+def test_update_hologram_non_blank(gpu, shape):
+    """An image already holding traps (src/move_traps.py:64-68 with a non-blank
+    black_image): angle(ifft2) through the device transform (complex64) vs the
+    float64 reference restatement, where the field is not near zero."""
+    from spatial_light_modulator_module_amd import move_traps as mt
+
+    rng = np.random.default_rng(11)
+    img = np.zeros(shape, np.uint8)
+    img[rng.integers(0, shape[0], 5), rng.integers(0, shape[1], 5)] = rng.integers(1, 256, 5)
+    y, x = 7, shape[1] - 3
+    want_img = img.copy()
+    ref = fo.update_hologram(want_img, [[y, x]], 0)
+    lit = img.astype(np.float64)
+    lit[y, x] = 255
+    field = np.fft.ifft2(lit)
+    keep = np.abs(field) > 1e-2 * np.abs(field).max()
+    got = mt.update_hologram(img, [[y, x]], 0)
+    assert got.dtype == np.float64 and got.shape == shape
+    err = wrapped(got, ref)[keep].max()
+    print(f"[parity] non-blank update_hologram {shape}: max wrapped phase error {err:.2e} on {keep.mean():.3f} of pixels")
+    assert err < 1e-3
+    np.testing.assert_array_equal(img, want_img)  # the trap pixel is back at 0, the rest untouched
+
+
+@pytest.mark.gpu
 def test_trap_phase_4096(gpu):
     from spatial_light_modulator_module_amd import _lib
 
