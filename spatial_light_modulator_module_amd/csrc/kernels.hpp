@@ -865,10 +865,13 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
 #pragma unroll
                 for (int m = 0; m < E; ++m)
                     v[l][m] = cv<V>(normalize(from_c64<C>(p.field_src[boff + PY * l + m * bstep]), ain_at(l, m)));
-            } else {
-#pragma unroll
-                for (int m = 0; m < E; ++m) v[l][m] = cv<V>(p.in[boff + PY * l + m * bstep]);
             }
+        }
+        if constexpr (MODE != ROW_PHASE_FWD && MODE != ROW_GD_INIT_FIELD) {
+#pragma unroll
+            for (int m = 0; m < E; ++m)  // slot-major, as the stores
+#pragma unroll
+                for (int l = 0; l < L; ++l) v[l][m] = cv<V>(p.in[boff + PY * l + m * bstep]);
         }
     };
     auto process = [&](long long tile, V (&v)[L][E], float (&)[1]) {
@@ -1002,16 +1005,20 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
                 fft_pair<K, true, false, C>(v, t, tw, lds, epi);
         }
         trace_point(trace, tile, 2, false);
+        // slot-major: the L rows of a thread are adjacent in a panel, so their pieces
+        // of one 128-B line leave back to back (a write-only probe of 8 x 4096^2:
+        // 32-B row pieces 571 us, adjacent row pairs 531 us with read, 1 GiB each way,
+        // whole lines 214 us; tools/row_store_probe.hip)
         if (p.wt) {  // uniform: one branch per tile, not per store
 #pragma unroll
-            for (int l = 0; l < L; ++l)
+            for (int m = 0; m < E; ++m)
 #pragma unroll
-                for (int m = 0; m < E; ++m) store_field(p.out + xoff + PX * l + m * bstep, cv<float2>(v[l][m]), 1);
+                for (int l = 0; l < L; ++l) store_field(p.out + xoff + PX * l + m * bstep, cv<float2>(v[l][m]), 1);
         } else {
 #pragma unroll
-            for (int l = 0; l < L; ++l)
+            for (int m = 0; m < E; ++m)
 #pragma unroll
-                for (int m = 0; m < E; ++m) p.out[xoff + PX * l + m * bstep] = cv<float2>(v[l][m]);
+                for (int l = 0; l < L; ++l) p.out[xoff + PX * l + m * bstep] = cv<float2>(v[l][m]);
         }
         trace_point(trace, tile, 3, true);
     };

@@ -19,15 +19,16 @@ def kernel_body(text, pat):
     end = text.find(".Lfunc_end", start)
     meta = {}
     name = m.group(1)
-    # metadata block lists ".name: <mangled>" with .vgpr_count etc. nearby
-    i = text.find(".name:           " + name)
-    if i < 0:
-        i = text.find(".name: " + name)
-    blk = text[max(0, i - 3000):i + 200] if i >= 0 else ""
-    for key in ("vgpr_count", "sgpr_count", "group_segment_fixed_size", "vgpr_spill_count", "agpr_count"):
-        mm = re.findall(r"\." + key + r":\s+(\d+)", blk)
+    # the kernel's own descriptor block (.amdhsa_kernel <name> ... .end_amdhsa_kernel):
+    # next_free_vgpr counts arch VGPRs + AGPRs (unified file; > 256 = one wave per SIMD)
+    i = text.find(".amdhsa_kernel " + name)
+    blk = text[i:text.find(".end_amdhsa_kernel", i)] if i >= 0 else ""
+    for key, out in (("next_free_vgpr", "vgpr_count"), ("next_free_sgpr", "sgpr_count"),
+                     ("group_segment_fixed_size", "group_segment_fixed_size"),
+                     ("private_segment_fixed_size", "scratch_bytes"), ("accum_offset", "accum_offset")):
+        mm = re.search(r"\.amdhsa_" + key + r"\s+(\d+)", blk)
         if mm:
-            meta[key] = int(mm[-1])
+            meta[out] = int(mm.group(1))
     return name, text[start:end], meta
 
 
