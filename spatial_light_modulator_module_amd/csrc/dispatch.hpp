@@ -14,8 +14,8 @@ using ColFn = void (*)(ColParams);
 #define SLM_DECLARE_LENGTH(N)                    \
     RowFn row_fn_##N(int mode, int prec, int lid);         \
     ColFn col_fn_##N(int cw, int mode, int tt, int prec, int lid); \
-    int row_threads_##N();                       \
-    int row_rpw_##N();                           \
+    int row_threads_##N(int prec);               \
+    int row_rpw_##N(int prec);                   \
     int col_threads_##N(int cw);
 
 SLM_DECLARE_LENGTH(0)
@@ -49,15 +49,15 @@ inline ColFn col_fn(int n, int cw, int mode, int tt, int prec, int lid = 0) {
     switch (n) { SLM_FOR_EACH_LENGTH(SLM_CASE) default: return nullptr; }
 #undef SLM_CASE
 }
-inline int row_threads(int n) {
+inline int row_threads(int n, int prec) {
 #define SLM_CASE(N) \
-    case N: return row_threads_##N();
+    case N: return row_threads_##N(prec);
     switch (n) { SLM_FOR_EACH_LENGTH(SLM_CASE) default: return 0; }
 #undef SLM_CASE
 }
-inline int row_rpw(int n) {
+inline int row_rpw(int n, int prec) {
 #define SLM_CASE(N) \
-    case N: return row_rpw_##N();
+    case N: return row_rpw_##N(prec);
     switch (n) { SLM_FOR_EACH_LENGTH(SLM_CASE) default: return 0; }
 #undef SLM_CASE
 }

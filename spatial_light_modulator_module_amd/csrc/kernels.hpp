@@ -150,8 +150,13 @@ constexpr int kLdsPair = 80 * 1024;
 #ifndef SLM_COL_LINES2_MIN_N
 #define SLM_COL_LINES2_MIN_N 4096  // 4096: col pass 715 -> 626 us for 8 x 4096^2 (twiddles cached again)
 #endif
+// Rows: two adjacent rows per thread of the float32 4096 narrow plan, their
+// pieces of each 128-B line loaded and stored back to back (slot-major): the
+// 8 x 4096^2 row pass 789-806 -> 688 us, 1 x 4096^2 neutral, phases bitwise
+// equal (profiles/r04/ab_rows_l2_s6.txt; 228 VGPRs, two workgroups per CU).
+// Float64 rows keep one row per thread (290 VGPRs with two: one wave per SIMD).
 #ifndef SLM_ROW_LINES2_MIN_N
-#define SLM_ROW_LINES2_MIN_N 8192  // off: 8 x 4096^2 row pass 695 -> 843 us with row pairs in-thread
+#define SLM_ROW_LINES2_MIN_N 4096
 #endif
 // Wave-local exchanges: where every thread of a line sits in one wave, a
 // Stockham exchange needs no workgroup barrier -- LDS writes, s_waitcnt, LDS
@@ -179,15 +184,18 @@ constexpr bool row_wave_local(int lines_per_thread) {
     return SLM_WAVE_LOCAL && lines_per_thread == 1 && (PlanOf<K>::T <= 16 || row_wave_remap<K>(lines_per_thread));
 }
 
-template <int K, bool COL>
+template <int K, bool COL, int P = PREC_F32>
 constexpr int lines_of() {
-    return (kPlans[K].variant == 1 && PlanOf<K>::N >= (COL ? SLM_COL_LINES2_MIN_N : SLM_ROW_LINES2_MIN_N)) ? 2 : 1;
+    return (kPlans[K].variant == 1 && PlanOf<K>::N >= (COL ? SLM_COL_LINES2_MIN_N : SLM_ROW_LINES2_MIN_N) &&
+            (COL || P == PREC_F32))
+               ? 2
+               : 1;
 }
 
-template <int K>  // plan key of the row length
+template <int K, int P = PREC_F32>  // plan key of the row length, precision
 struct RowCfg {
     static constexpr int T = PlanOf<K>::T;
-    static constexpr int L = lines_of<K, false>();  // rows per thread
+    static constexpr int L = lines_of<K, false, P>();  // rows per thread
     // rows per workgroup: a row quad (whole 128-B lines of the blocked layout),
     // or a row pair when a quad would not leave room for two workgroups per CU
     // and a pair still fills 8 waves (the partner pair, which reads the other
@@ -759,26 +767,26 @@ constexpr bool kShuffle = SLM_SHUFFLE && P == PREC_F32 && PlanOf<K>::N == kShufN
 
 template <int K, int P>
 constexpr int row_wpe() {
-    using X = XchgOf<P, (long long)RowCfg<K>::RPW * PlanOf<K>::ROWSTRIDE, K>;
+    using X = XchgOf<P, (long long)RowCfg<K, P>::RPW * PlanOf<K>::ROWSTRIDE, K>;
     // per-plan waves-per-SIMD floor for the float32 row kernels (register budget
     // 512 / w; A/B knob: -DSLM_ROW_WPE_K=<key> -DSLM_ROW_WPE=<w>)
 #if defined(SLM_ROW_WPE_K) && defined(SLM_ROW_WPE)
     if constexpr (K == SLM_ROW_WPE_K && P == 0) return SLM_ROW_WPE;
 #endif
-    return occupancy_wpe(RowCfg<K>::THREADS,
-                         (kLdsDouble<K, false> ? 2 : 1) * (long long)RowCfg<K>::RPW * PlanOf<K>::ROWSTRIDE * sizeof(X));
+    return occupancy_wpe(RowCfg<K, P>::THREADS,
+                         (kLdsDouble<K, false> ? 2 : 1) * (long long)RowCfg<K, P>::RPW * PlanOf<K>::ROWSTRIDE * sizeof(X));
 }
 
 template <int K, int MODE, int P, int LID>
-__global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_kernel(RowParams p) {
+__global__ void __launch_bounds__((RowCfg<K, P>::THREADS), (row_wpe<K, P>())) row_kernel(RowParams p) {
     constexpr int LAYOUT_X = LayoutOf<LID>::X, LAYOUT_Y = LayoutOf<LID>::Y;
     using C = CplxOf<P>;
     using S = Scalar<C>;
     constexpr int W = PlanOf<K>::N;
     constexpr int E = PlanOf<K>::E;
     constexpr int T = PlanOf<K>::T;
-    constexpr int RPW = RowCfg<K>::RPW;
-    constexpr int L = RowCfg<K>::L;
+    constexpr int RPW = RowCfg<K, P>::RPW;
+    constexpr int L = RowCfg<K, P>::L;
     constexpr int LINE = PlanOf<K>::ROWSTRIDE;
     constexpr int TL = T < 16 ? T : 16;
     using X = XchgOf<P, (long long)RPW * LINE, K>;
@@ -786,7 +794,7 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
     constexpr int ALT = kLdsDouble<K, false> ? RPW * LINE : 0;
     // wave-shuffle pair for 4096-point rows (fft_shuffle.hpp; float32 GS, one row per workgroup)
     constexpr bool SHUF4 = kShuffle4096<K, P> && MODE == ROW_GS_MAIN && RPW == 1 && L == 1 &&
-                           RowCfg<K>::THREADS == 256 && std::is_same_v<X, float2>;
+                           RowCfg<K, P>::THREADS == 256 && std::is_same_v<X, float2>;
     constexpr int SMEM_ROW = (ALT ? 2 : 1) * RPW * LINE;
     __shared__ X smem[SHUF4 && SMEM_ROW < 2 * kShuf4N ? 2 * kShuf4N : SMEM_ROW];
 
@@ -795,8 +803,8 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
     // touches 16 consecutive x of 4 rows = four whole 128-B lines of the
     // blocked layout, and a 16-lane LDS write group stays inside one row. A
     // thread carries rows lrow * L + l, l < L.
-    constexpr int QR = RowCfg<K>::QR;
-    constexpr bool WV = RowCfg<K>::kWave;
+    constexpr int QR = RowCfg<K, P>::QR;
+    constexpr bool WV = RowCfg<K, P>::kWave;
     // wave-shuffle pair: lane bit 0 selects the row of the pair, t per fft_shuffle.hpp
     constexpr bool SHUF =
         kShuffle<K, P> && (MODE == ROW_GS_MAIN || MODE == ROW_GD_MAIN || MODE == ROW_GD_LIN) && RPW == 2 && L == 1;
@@ -804,7 +812,7 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
     if constexpr (SHUF) {
         t = shuffle_t(threadIdx.x);
         lrow = threadIdx.x & 1;
-    } else if constexpr (RowCfg<K>::kRemap) {  // wave-line: T consecutive lanes per row, rows never cross a wave
+    } else if constexpr (RowCfg<K, P>::kRemap) {  // wave-line: T consecutive lanes per row, rows never cross a wave
         t = threadIdx.x % T;
         lrow = threadIdx.x / T;
     } else {
@@ -819,7 +827,7 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
     const LdsLine<X, WV ? 0 : ALT, WV> lds{smem + lrow * LINE, LINE};
     if constexpr (MODE == ROW_GS_MAIN || MODE == ROW_GD_MAIN || MODE == ROW_GD_LIN) trace_entry(p.trace);
     sgpr_pin(p.in, p.out, p.holo, p.H, p.B, p.ntile, p.tw, p.ain, p.wt, gridDim.x);
-    Twiddles<K, C, tw_mode<P, RowCfg<K>::THREADS, K, false>()> tw;
+    Twiddles<K, C, tw_mode<P, RowCfg<K, P>::THREADS, K, false>()> tw;
     static_assert(!SHUF || (std::is_same_v<X, float2> && sizeof(smem) >= 4 * kShufN * sizeof(float2)),
                   "the shuffle pair needs two 2-line complex64 exchange buffers");
     ShuffleTw stw;
@@ -967,8 +975,8 @@ __global__ void __launch_bounds__(RowCfg<K>::THREADS, (row_wpe<K, P>())) row_ker
             {
                 const double* gm = p.gmax + ((long long)b * p.max_loops + p.iter) * p.nwg_col;
                 double mx = 0.0;
-                for (int k = threadIdx.x; k < p.nwg_col; k += RowCfg<K>::THREADS) mx = fmax(mx, gm[k]);
-                block_reduce_max<RowCfg<K>::THREADS>(mx);
+                for (int k = threadIdx.x; k < p.nwg_col; k += RowCfg<K, P>::THREADS) mx = fmax(mx, gm[k]);
+                block_reduce_max<RowCfg<K, P>::THREADS>(mx);
                 if (threadIdx.x == 0) smax = mx;
                 lds_barrier();
             }

@@ -103,8 +103,12 @@ ColFn SLM_PASTE(col_fn_, SLM_N)(int cw, int mode, int tt, int prec, int lid) {
     return nullptr;
 }
 
-int SLM_PASTE(row_threads_, SLM_N)() { return RowCfg<SLM_N>::THREADS; }
-int SLM_PASTE(row_rpw_, SLM_N)() { return RowCfg<SLM_N>::RPW; }
+int SLM_PASTE(row_threads_, SLM_N)(int prec) {
+    return prec == PREC_F64 ? RowCfg<SLM_N, PREC_F64>::THREADS : RowCfg<SLM_N, PREC_F32>::THREADS;
+}
+int SLM_PASTE(row_rpw_, SLM_N)(int prec) {
+    return prec == PREC_F64 ? RowCfg<SLM_N, PREC_F64>::RPW : RowCfg<SLM_N, PREC_F32>::RPW;
+}
 int SLM_PASTE(col_threads_, SLM_N)(int cw) {
     switch (cw) {
         case 1: return ColCfg<SLM_N, 1>::THREADS;

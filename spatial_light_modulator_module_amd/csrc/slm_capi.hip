@@ -464,8 +464,8 @@ int configure(slm_plan* p, int prec) {
     p->cw = cw;
     p->nwg = p->W / cw;
     p->col_threads = col_threads(col_key, cw);
-    p->row_threads = row_threads(row_key);
-    p->rpw = row_rpw(row_key);
+    p->row_threads = row_threads(row_key, prec);
+    p->rpw = row_rpw(row_key, prec);
     p->tw_row = tr;
     p->tw_col = tc;
     return 0;

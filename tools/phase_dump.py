@@ -3,7 +3,7 @@
 save the phases, for bitwise A/B checks between builds that must not change the
 arithmetic (layouts, access order, register budgets).
 
-    python tools/phase_dump.py <n> <batch> <iters> <out.npy>
+    python tools/phase_dump.py <n> <batch> <iters> <out.sha>
 """
 import os
 import sys
@@ -24,7 +24,10 @@ def main():
         p.run(iters, 0.0, False)
         ph, e, stats, _ = p.read()
         print(f"{os.path.basename(_lib.LIB_PATH)} {n}x{n}x{b}: engine {p.engine()} info {p.info()}")
-    np.save(out, ph)
+    # a digest, not the array (a 4096^2 batch is 128 MiB; gpurun_out copies back <= 64 MiB)
+    import hashlib
+    with open(out, "w") as f:
+        f.write(hashlib.sha256(np.ascontiguousarray(ph).tobytes()).hexdigest() + "\n")
 
 
 if __name__ == "__main__":

@@ -156,6 +156,30 @@ __global__ void __launch_bounds__(256) pair_copy(const float2* __restrict__ in, 
         for (int r = 0; r < 2; ++r) out[hoff + blk(y + r, t + 256 * m)] = v[r][m];
 }
 
+// column tiles of the 4096 column pass (csrc/kernels.hpp col_kernel, two columns per
+// thread): W columns of one 4-wide panel per workgroup, thread t at y = t + 256 m,
+// 8 W bytes per (y, tile) -- W = 2: 16 B of every 32-B panel row (the shipped
+// 2-column tile), W = 4: the whole panel row (a contiguous 128-KB stream)
+template <int W>
+__global__ void __launch_bounds__(256) col_copy(const float2* __restrict__ in, float2* __restrict__ out) {
+    constexpr int TPP = 4 / W;  // tiles per panel
+    const int id = xcd_remap(blockIdx.x, gridDim.x);
+    const int per_holo = (N / 4) * TPP;
+    const long long hoff = (long long)(id / per_holo) * N * N;
+    const int r = id % per_holo, panel = r / TPP, c0 = (r % TPP) * W, t = threadIdx.x;
+    const long long base = hoff + (long long)panel * N * 4 + c0;
+    float4 v[16][W / 2];
+#pragma unroll
+    for (int m = 0; m < 16; ++m)
+#pragma unroll
+        for (int k = 0; k < W / 2; ++k) v[m][k] = *reinterpret_cast<const float4*>(in + base + (t + 256 * m) * 4 + 2 * k);
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int m = 0; m < 16; ++m)
+#pragma unroll
+        for (int k = 0; k < W / 2; ++k) *reinterpret_cast<float4*>(out + base + (t + 256 * m) * 4 + 2 * k) = v[m][k];
+}
+
 int main() {
     for (int B : {1, 8}) {
         const size_t bytes = (size_t)B * N * N * sizeof(float2);
@@ -190,6 +214,8 @@ int main() {
         run(write_only<false>, grid, "wr_x2");
         run(write_only<true>, grid, "wr_quad");
         run(pair_copy, grid / 2, "pair");
+        run(col_copy<2>, B * N / 2, "col2");
+        run(col_copy<4>, B * N / 4, "col4");
         (void)hipFree(a);
         (void)hipFree(b);
     }
