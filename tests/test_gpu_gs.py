@@ -108,6 +108,42 @@ def test_gs_4096_property(gpu):
 
 
 @pytest.mark.gpu
+def test_4096_rows_incoming_amplitude_and_gd(gpu):
+    """The float32 4096 row kernels carry two adjacent rows per thread (r04):
+    the modes that read per-row data beside the field -- a_in in the GS
+    projection (uint8 target) and the GD field update -- against the float64
+    restatement from a random start, 3 iterations each."""
+    from spatial_light_modulator_module_amd import algorithms as alg
+
+    n = 4096
+    rng = np.random.default_rng(40962)
+    t = rng.integers(0, 256, (n, n)).astype(np.uint8)
+    inten = rng.uniform(0.25, 2.0, (n, n))
+    ain = np.sqrt(inten).astype(np.float32)
+    phi0 = rng.uniform(-np.pi, np.pi, (n, n)).astype(np.float32)
+    phase, _, errs, _, _ = alg.run_gs(t[None], 3, ain=ain, initial_phase=phi0[None])
+    ph_o, _, err_o = orc.gerchberg_saxton_faithful(t, 3, incoming_intensity=ain.astype(np.float64) ** 2,
+                                                   initial_phase=phi0)
+    rms = orc.phase_rms(phase[0], ph_o)
+    print(f"[parity] GS 4096^2 uint8 with a_in, random phase x3 vs float64: phase rms {rms:.3e}")
+    assert rms < PHASE_RMS_TOL
+    np.testing.assert_allclose(errs[0], err_o, rtol=1e-5)
+    alg.clear_plans()
+
+    tf = rng.uniform(0, 255, (n, n)).astype(np.float32)
+    x0 = alg.make_initial_guess("random", None, tf, 42)
+    loops = 3
+    rates = np.full(loops, 0.005)
+    ph, _, errs, _, _ = alg.run_gd(tf[None], loops, rates, 1.0, initial_field=x0[None])
+    ref, _, ref_err, _ = orc.gradient_descent_faithful(tf, loops, 0.005, 1.0, 0, initial_field=x0)
+    rms = orc.phase_rms(ph[0], ref)
+    print(f"[parity] GD 4096^2 random guess x{loops} vs float64: phase rms {rms:.3e}")
+    assert rms < PHASE_RMS_TOL
+    np.testing.assert_allclose(errs[0], ref_err, rtol=1e-5)
+    alg.clear_plans()
+
+
+@pytest.mark.gpu
 def test_gs_batch_equals_single(gpu):
     from spatial_light_modulator_module_amd import algorithms as alg
 
