@@ -1550,24 +1550,41 @@ __global__ void __launch_bounds__(256) field_phase_kernel(const float2* field, f
 // B), 256 threads; H and W are multiples of 64 for every supported side.
 template <int PLOG>
 __global__ void __launch_bounds__(256) unblock_tile_kernel(const float* in, float* out, int H, int W) {
+    // 64 x 64 tiles; vector accesses both ways: panel rows in (VW = min(P, 4)
+    // floats per lane), 16-B row pieces out (sides are multiples of 64)
     constexpr int P = 1 << PLOG;
-    __shared__ float tile[64][65];
+    constexpr int VW = P < 4 ? P : 4;
+    constexpr int LD = 68;  // row stride: 16-B aligned rows for ds_read_b128
+    __shared__ __attribute__((aligned(16))) float tile[64 * LD];
     const long long holo = (long long)H * W;
     const int x0 = blockIdx.x * 64, y0 = blockIdx.y * 64;
     const float* src = in + blockIdx.z * holo;
     float* dst = out + blockIdx.z * holo;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const int i = threadIdx.x + 256 * k;  // panel-major order of the tile: (q, yy, xx)
-        const int xx = i & (P - 1), yy = (i >> PLOG) & 63, q = i >> (PLOG + 6);
-        tile[yy][q * P + xx] = src[(((long long)(x0 >> PLOG) + q) * H + y0 + yy) * P + xx];
+    for (int k = 0; k < 16 / VW; ++k) {
+        const int e = (threadIdx.x + 256 * k) * VW;  // panel-major order of the tile: (q, yy, xx)
+        const int xx = e & (P - 1), yy = (e >> PLOG) & 63, q = e >> (PLOG + 6);
+        const float* s0 = src + (((long long)(x0 >> PLOG) + q) * H + y0 + yy) * P + xx;
+        float* t0 = tile + yy * LD + q * P + xx;
+        if constexpr (VW == 4) {
+            const float4 v = *reinterpret_cast<const float4*>(s0);
+            t0[0] = v.x;
+            t0[1] = v.y;
+            t0[2] = v.z;
+            t0[3] = v.w;
+        } else {
+            const float2 v = *reinterpret_cast<const float2*>(s0);
+            t0[0] = v.x;
+            t0[1] = v.y;
+        }
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
+    for (int k = 0; k < 4; ++k) {
         const int i = threadIdx.x + 256 * k;
-        const int yy = i >> 6, xx = i & 63;
-        dst[(long long)(y0 + yy) * W + x0 + xx] = tile[yy][xx];
+        const int yy = i >> 4, xx = (i & 15) * 4;
+        *reinterpret_cast<float4*>(dst + (long long)(y0 + yy) * W + x0 + xx) =
+            *reinterpret_cast<const float4*>(tile + yy * LD + xx);
     }
 }
 
