@@ -285,7 +285,21 @@ def main():
     if world > 1 and opt.gpus not in (1, world):
         print(f"bench.py: --gpus {opt.gpus} but the launcher started {world} ranks; using {world}", file=sys.stderr)
     group = parallel.Group.from_env()
-    _lib.init(local_rank if world > 1 else int(os.environ.get("SLM_DEVICE", "0")))
+    if world == 1:
+        _lib.init(int(os.environ.get("SLM_DEVICE", "0")))
+    else:
+        # every rank must have its GPU before any waits in ncclCommInitRank for the
+        # others (a rank that failed here would leave the rest blocked in RCCL)
+        try:
+            _lib.init(local_rank)
+            err = None
+        except Exception as e:  # noqa: BLE001 -- reported by every rank, then all exit
+            err = f"rank {rank}: {e}"
+        errs = [e for e in group.all_gather(err) if e]
+        if errs:
+            print("bench.py: device initialisation failed: " + "; ".join(errs), file=sys.stderr)
+            group.close()
+            sys.exit(1)
     n, bper, iters = opt.size, opt.batch_per_gpu, opt.iters
     counts = [bper] * world
 

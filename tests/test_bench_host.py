@@ -71,7 +71,7 @@ class _FakePlan:
         pass
 
 
-def _fake_lib(rank):
+def _fake_lib(rank, fail_init=False):
     from spatial_light_modulator_module_amd import _lib as real
 
     class Fake:
@@ -83,7 +83,8 @@ def _fake_lib(rank):
 
         @staticmethod
         def init(device=None):
-            pass
+            if fail_init:
+                raise real.SlmError(f"slm_init({device}) failed (-1): device {device} outside [0, 1)")
 
         @staticmethod
         def Plan(*a):
@@ -96,6 +97,8 @@ def _fake_lib(rank):
         @staticmethod
         def comm_init(n, r, uid):
             assert len(uid) == 128
+            if os.environ.get("BENCH_TEST_NO_COMM"):
+                raise AssertionError("comm_init reached after a rank failed its device initialisation")
 
         @staticmethod
         def comm_destroy():
@@ -112,13 +115,15 @@ def _fake_lib(rank):
     return Fake
 
 
-def _rank(rank, world, port, out):
+def _rank(rank, world, port, out, fail_rank=-1):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port), SLM_RDZV_PORT=str(port), SLM_JOB_TOKEN="bench-host-test")
+    if fail_rank >= 0:
+        os.environ["BENCH_TEST_NO_COMM"] = "1"
     sys.path.insert(0, ROOT)
     import bench
 
-    bench._lib = _fake_lib(rank)
+    bench._lib = _fake_lib(rank, fail_init=rank == fail_rank)
     sys.argv = ["bench.py", "--gpus", str(world), "--steps", "3", "--warmup", "1", "--size", "64", "--iters", "10",
                 "--batch-per-gpu", "2"]
     with open(out, "w") as f:
@@ -156,3 +161,20 @@ def test_bench_two_ranks_json_shape(tmp_path):
     assert ranks[0]["gather_bytes_to_root"] == 0 and ranks[1]["gather_bytes_to_root"] == 2 * 64 * 64 * 4
     for d in ranks:
         assert d["step_ms"] > 0 and d["gather_ms"] == 0.25 and set(d["kernel_avg_us"]) == {"col_main", "row_main"}
+
+
+def test_bench_rank_without_device_stops_every_rank(tmp_path):
+    """A rank whose GPU fails to initialise makes every rank exit with an error
+    before any of them enters RCCL's communicator set-up (where the others
+    would otherwise wait for it indefinitely)."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, str(tmp_path / f"r{r}.out"), 1)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 1
+    assert not [ln for ln in (tmp_path / "r0.out").read_text().splitlines() if ln.startswith("{")]
