@@ -55,6 +55,35 @@ def test_gd_tolerance_stop_at_odd_iteration(gpu, n):
 
 
 @pytest.mark.gpu
+def test_gs_4096_batch_with_different_stop_iterations(gpu):
+    """The float32 4096 row kernels carry two rows per thread (r04): a checked
+    run whose two holograms stop after 3 and 5 iterations (tiles of a stopped
+    hologram leave before their exchanges) against the threaded float64
+    restatement with the same tolerance."""
+    from oracle import fast_f64
+    from spatial_light_modulator_module_amd import algorithms as alg
+
+    n = 4096
+    rng = np.random.default_rng(34)
+    base = rng.uniform(0, 255, (n, n))
+    phi0 = rng.uniform(-np.pi, np.pi, base.shape).astype(np.float32)
+    _, _, err_base = fast_f64.gerchberg_saxton_f64(base.astype(np.float32), 8, initial_phase=phi0)
+    tol = 1000.0
+    stops = (2, 4)
+    scales = [np.sqrt(tol / _tol_between(err_base, s)) for s in stops]
+    t = np.stack([(c * base).astype(np.float32) for c in scales])
+    ph, _, errs, _, _ = alg.run_gs(t, 8, tol=tol, initial_phase=np.stack([phi0] * 2))
+    for k, s in enumerate(stops):
+        ref_ph, _, ref_err = fast_f64.gerchberg_saxton_f64(t[k], 8, initial_phase=phi0, tolerance=tol)
+        assert len(errs[k]) == len(ref_err) == s + 1, (k, len(errs[k]), len(ref_err))
+        np.testing.assert_allclose(errs[k], ref_err, rtol=1e-4)
+        rms = orc.phase_rms(ph[k], ref_ph)
+        print(f"[parity] GS 4096^2 checked batch, hologram {k} stops after {s + 1}: phase rms {rms:.3e}")
+        assert rms < 1e-5
+    alg.clear_plans()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n", [128, 1024])
 def test_gs_batch_with_different_stop_iterations(gpu, n):
     """One tolerance, three holograms scaled so that each stops at a different
