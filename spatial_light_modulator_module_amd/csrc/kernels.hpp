@@ -1014,9 +1014,9 @@ __global__ void __launch_bounds__((RowCfg<K, P>::THREADS), (row_wpe<K, P>())) ro
         }
         trace_point(trace, tile, 2, false);
         // slot-major: the L rows of a thread are adjacent in a panel, so their pieces
-        // of one 128-B line leave back to back (a write-only probe of 8 x 4096^2:
-        // 32-B row pieces 571 us, adjacent row pairs 531 us with read, 1 GiB each way,
-        // whole lines 214 us; tools/row_store_probe.hip)
+        // of one 128-B line leave back to back (tools/row_store_probe.hip, a copy of
+        // 8 x 4096^2 in the row pass's shapes: 32-B row pieces 711 us, adjacent row
+        // pairs 531 us, whole lines 445 us)
         if (p.wt) {  // uniform: one branch per tile, not per store
 #pragma unroll
             for (int m = 0; m < E; ++m)
