@@ -158,3 +158,38 @@ def test_generic_intensity_vs_numpy(gpu):
     got = gpu.fft2_intensity(ph)
     want = np.abs(np.fft.fft2(np.exp(1j * ph.astype(np.float64)))) ** 2
     np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-5 * float(want.max()))
+
+
+@pytest.mark.gpu
+def test_generic_incoming_amplitude_gs_and_gd(gpu):
+    """An incoming intensity (src/algorithms.py:14-19 / :65-70) on a shape with
+    no radix plan: GS (uint8 target, warm start) and GD (float32 target, random
+    guess scaled by a_in) against the faithful float64 oracle."""
+    from spatial_light_modulator_module_amd import algorithms as alg
+
+    shape = (90, 150)
+    rng = np.random.default_rng(12)
+    ain = np.sqrt(rng.uniform(0.25, 2.0, shape)).astype(np.float32)  # a_in; the oracle gets a_in^2 as the image
+    inten = ain.astype(np.float64) ** 2
+    t = _target(shape, True, seed=13)
+    # SURVEY.md 8c warm-start protocol: the reference's phase after 30 cold iterations
+    phi30, _, _ = orc.gerchberg_saxton_faithful(t, 30, incoming_intensity=inten)
+    phi30 = phi30.astype(np.float32)
+    ph, _, errs, _, _ = alg.run_gs(t[None], 30, ain=ain, initial_phase=phi30[None])
+    ref, _, ref_err = orc.gerchberg_saxton_faithful(t, 30, incoming_intensity=inten, initial_phase=phi30)
+    rms = orc.phase_rms(ph[0], ref)
+    print(f"[parity] DFT-GEMM GS {shape} uint8 with a_in, warm 30+30: phase rms {rms:.3e}")
+    assert rms < 1e-6
+    np.testing.assert_allclose(errs[0], ref_err, rtol=1e-6)
+
+    tf = _target(shape, False, seed=14)
+    x0 = alg.make_initial_guess("random", inten ** 0.5, tf, 42)
+    loops = 40
+    ph, _, errs, _, _ = alg.run_gd(tf[None], loops, np.full(loops, 0.005), 1.0, ain=ain, initial_field=x0[None])
+    ref, _, ref_err, _ = orc.gradient_descent_faithful(tf, loops, 0.005, 1.0, 0, incoming_intensity=inten,
+                                                       initial_field=x0)
+    rms = orc.phase_rms(ph[0], ref)
+    print(f"[parity] DFT-GEMM GD {shape} with a_in, {loops} iterations: phase rms {rms:.3e}")
+    assert rms < 1e-5  # the complex64 initial field crossing the C-ABI, as test_generic_gd_vs_oracle
+    np.testing.assert_allclose(errs[0], ref_err, rtol=1e-5)
+    alg.clear_plans()
