@@ -188,6 +188,26 @@ def cpu_baseline(n: int, iters: int, budget_s: float):
             "ms_per_iter": per_iter * 1e3, "host_cpus": os.cpu_count()}
 
 
+def cpu_baseline_configs0(reps: int = 3):
+    """BASELINE.json configs[0]: GS on one 256x256 random target, 50 iterations,
+    the NumPy CPU path (the faithful float64 restatement, oracle/gs_gd_oracle.py,
+    single-threaded like the reference) -- whole runs timed, not extrapolated."""
+    from oracle import gs_gd_oracle as orc
+
+    t = targets(0, 1, 256)[0]
+    orc.gerchberg_saxton_faithful(t, 50)  # warm-up (imports, FFT plan caches)
+    walls = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        orc.gerchberg_saxton_faithful(t, 50)
+        walls.append(time.perf_counter() - t0)
+    wall = min(walls)
+    return {"value": 1.0 / wall, "unit": "holograms/s", "cores": 1, "kind": "port",
+            "sample": f"{reps} whole 50-iteration GS runs (best of) of the float64 restatement on one 256x256 "
+                      "float32 target (BASELINE.json configs[0])",
+            "s_per_hologram": wall, "ms_per_iter": wall / 50 * 1e3, "host_cpus": os.cpu_count()}
+
+
 def cpu_baseline_all_cores(n: int, iters: int, budget_s: float):
     """The multi-threaded float64 restatement (oracle/fast_f64.py: pocketfft and
     element-wise work over the host share's threads) on the same target."""
@@ -435,6 +455,7 @@ def main():
     if world == 1 and not opt.no_extra:
         extra = {"pcie_inclusive": pcie_inclusive(plan, targets(0, bper, n), iters)}
         try:  # every line at its BASELINE.json config's own iteration count
+            extra["gs_256_it50"] = secondary(256, 1, 50, reps=20)  # configs[0]'s workload on the GPU
             extra["gs_4096"] = secondary(4096, 1, 200)  # north-star shape, one hologram
             extra["gs_4096_batch8"] = secondary(4096, 8, 200)  # configs[4] per GPU at 8 GPUs
             extra["gs_1024_batch64"] = secondary(1024, 64, 200)  # configs[3] per GPU at 8 GPUs
@@ -448,6 +469,7 @@ def main():
     if world == 1 and not opt.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, iters, opt.cpu_sample_seconds)
         out["cpu_baseline_all_cores"] = cpu_baseline_all_cores(n, iters, opt.cpu_sample_seconds / 2)
+        out["cpu_baseline_configs0"] = cpu_baseline_configs0()
     print(json.dumps(out), flush=True)
     plan.close()
     if world > 1:

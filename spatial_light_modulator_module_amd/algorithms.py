@@ -24,6 +24,7 @@ from __future__ import annotations
 import collections
 import os
 import sys
+import warnings
 
 import numpy as np
 
@@ -196,6 +197,10 @@ def run_gs_multi(targets, loops, devices, tol=0.0, ain=None):
     then report the same error_evolution)."""
     t = np.asarray(targets)
     if _needs_exact_stats(t):
+        if len(set(int(d) for d in devices)) > 1:
+            warnings.warn(f"{t.dtype} targets are not exact in float32: the batch runs on this process's one "
+                          f"GPU (run_gs) so the error keeps its float64 terms; `devices` {list(devices)} is "
+                          "ignored -- pass uint8 or float32 frames to shard them", RuntimeWarning, stacklevel=2)
         return run_gs(t, loops, tol, ain)
     tdev, _ = target_for_device(t)
     phase, e, stats, iters = _lib.gs_multi(tdev, loops, devices, tol=tol, ain=ain)

@@ -80,6 +80,7 @@ struct ColParams {
     int nwg;                 // column workgroups per hologram (W / CW)
     long long holo;          // elements per hologram
     float wa;                // GD white_attention
+    float stat_k;            // GS: power of two ~ 1/holo^2 scaling E^2 in the float32 partial sums (no overflow)
     const void* tw;          // twiddle table for length H (float2 or double2)
     unsigned long long* trace;  // SLM_TRACE builds: [tile][8] phase timestamps (kTraceSlots)
     int B;                   // holograms
@@ -1404,14 +1405,18 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P, M
             // partial, averaging out over the hologram's partials (the error's
             // expansion cancels by ~1e2 late in a run: error curves still
             // agree to ~1e-6 relative, gated at 1e-4)
+            // E^2 is summed scaled by stat_k (a power of two ~ 1/holo^2: the same
+            // bits, and no float32 overflow for a bright incoming amplitude whose
+            // energy sits in a few pixels -- E reaches (holo a_in)^2)
             float mxf = 0.f, s2f = 0.f, stf = 0.f;
+            const float stat_k = MODE == COL_GS_MAIN ? p.stat_k : 1.f;
             auto epi = [&](int l, int m, C& z) {
                 const S e = z.x * z.x + z.y * z.y;
                 const float tl = tv[l][m];
                 if constexpr (MODE == COL_GS_MAIN) {
                     const float ef = (float)e;  // |C|^2 as the reference's float64 expected_outcome sees it
                     mxf = fmaxf(mxf, ef);
-                    s2f = fmaf(ef, ef, s2f);
+                    s2f = fmaf(ef * stat_k, ef, s2f);
                     stf = fmaf(ef, TgtLoad<TT>::intensity(tl), stf);
                 } else if constexpr (MODE == COL_GD_STATS) {
                     const double ed = (double)(float)e;
@@ -1447,7 +1452,7 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P, M
             // the cross-lane statistics reduction (LDS only) runs while the field stores drain
             if constexpr (MODE == COL_GS_MAIN) {
                 mx = mxf;
-                s2 = s2f;
+                s2 = (double)s2f / (double)stat_k;  // exact: a power of two
                 st = stf;
             }
             if constexpr (MODE == COL_GS_MAIN || MODE == COL_GD_STATS) {

@@ -320,6 +320,8 @@ struct slm_plan {
     int gd_mode = GD_AUTO;
     int skip_wg_plus1 = 0;  // $SLM_GD_FAULT_TEST: fused-path fault injection (tests)
     int gd_recoveries = 0;  // runs redone on the two-launch path after a grid fault
+    bool fused_pending = false;  // a one-launch GD run is queued and its fault flag not read yet
+    bool ran = false;            // a run was enqueued (the state buffers hold something)
     float2* field0 = nullptr;  // GD: host-set initial field (blocked), never overwritten by a run
     bool field_fresh = false;  // set_field since the last run: the plan's field is field0
     // parameters of the last enqueued run (a grid fault reruns it)
@@ -526,6 +528,7 @@ ColParams col_params(slm_plan* p) {
     c.W = p->W;
     c.nwg = p->nwg;
     c.holo = p->holo;
+    c.stat_k = std::ldexp(1.0f, -2 * (int)std::ceil(std::log2((double)p->holo)));
     c.tw = p->tw_col;
     c.wt = p->wt_col;
     c.trace = p->trace_col;
@@ -789,6 +792,7 @@ int enqueue_gd(slm_plan* p, int loops, double tol, int checked, float wa) {
 int recover_grid_fault(slm_plan* p, bool* faulted) {
     *faulted = false;
     if (!p->gfault) return 0;
+    p->fused_pending = false;  // the caller drained the stream: the flag below covers every queued run
     int f = 0;
     RC(copy_sync(&f, p->gfault, sizeof(int), hipMemcpyDeviceToHost, p->stream));
     if (!f) return 0;
@@ -839,6 +843,7 @@ int enqueue_run(slm_plan* p, int loops, double tol, int checked, float wa) {
     if (p->algo == SLM_ALGO_GD && !p->lr_set) return fail(SLM_ERR_STATE, "learning rates not set");
     HIP_TRY(hipSetDevice(p->device));
     p->field_fresh = false;  // the run writes the field
+    p->ran = true;
     RC(launch(p, SLM_KERNEL_OTHER, fill_int_kernel, dim3((p->B + 255) / 256), dim3(256), p->stop, p->B,
               (int)INT_MAX));
     if (p->gen)
@@ -1242,7 +1247,11 @@ int slm_plan_run(slm_plan* p, int loops, double tol, int checked, float wa) {
         const char* e = std::getenv("SLM_GRAPH");
         return !e || std::atoi(e) != 0;
     }();
-    if (!p || !use_graph || p->gen) return enqueue_run(p, loops, tol, checked, wa);  // rocBLAS calls: not captured
+    if (!p || !use_graph || p->gen) {  // rocBLAS calls: not captured
+        RC(enqueue_run(p, loops, tol, checked, wa));
+        if (p && p->gfault && gd_fused_fn(p, checked)) p->fused_pending = true;
+        return 0;
+    }
     const int state = (p->phase_set ? 1 : 0) | (p->field_set ? 2 : 0);
     if (!p->gexec || p->g_state != state || p->g_loops != loops || p->g_tol != tol || p->g_checked != checked || p->g_wa != wa) {
         HIP_TRY(hipSetDevice(p->device));
@@ -1272,6 +1281,7 @@ int slm_plan_run(slm_plan* p, int loops, double tol, int checked, float wa) {
     }
     HIP_TRY(hipSetDevice(p->device));
     HIP_TRY(hipGraphLaunch(p->gexec, p->stream));
+    if (p->gfault && gd_fused_fn(p, checked)) p->fused_pending = true;
     return 0;
 }
 
@@ -1625,6 +1635,7 @@ int slm_plan_read_field(slm_plan* p, float* field) {
     if (!p || !field) return fail(SLM_ERR_ARG, "null argument");
     if (p->algo != SLM_ALGO_GD) return fail(SLM_ERR_STATE, "the field is the state of GD plans");
     HIP_TRY(hipSetDevice(p->device));
+    if (!p->field_fresh && !p->ran) return fail(SLM_ERR_STATE, "no field yet: neither set_field nor a run");
     const long long n = (long long)p->B * p->holo;
     if (p->gen) {
         const float2* src = p->field0;
@@ -1707,8 +1718,10 @@ int gather_slab(slm_plan* p, const void* src, long long per_item, size_t elem, n
     if (root < 0 || root >= n) return fail(SLM_ERR_ARG, "root %d outside [0, %d)", root, n);
     if (counts[me] != p->B) return fail(SLM_ERR_ARG, "counts[%d]=%d but the plan holds %d", me, counts[me], p->B);
     // a GD run on the one-launch column side may have faulted (its grid wait gave
-    // up): settle it -- redo it on two launches -- before its results leave this rank
-    if (p->gfault) RC(slm_plan_sync(p));
+    // up): settle it -- redo it on two launches -- before its results leave this
+    // rank. Only a fused run queued since the last check can have (no host sync
+    // per gather otherwise)
+    if (p->fused_pending) RC(slm_plan_sync(p));
     std::vector<long long> off(n + 1);
     RC(slm_gather_layout(n, counts, per_item, off.data()));
     if (me == root) {

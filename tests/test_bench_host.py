@@ -178,3 +178,16 @@ def test_bench_rank_without_device_stops_every_rank(tmp_path):
         p.join(120)
         assert p.exitcode == 1
     assert not [ln for ln in (tmp_path / "r0.out").read_text().splitlines() if ln.startswith("{")]
+
+
+def test_cpu_baseline_configs0_times_whole_runs():
+    """BASELINE.json configs[0] (GS 256^2, 50 iterations, the NumPy CPU path)
+    is timed as whole runs of the float64 restatement, with the host's CPU
+    count stated."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    cb = bench.cpu_baseline_configs0(reps=1)
+    assert cb["unit"] == "holograms/s" and cb["cores"] == 1 and cb["kind"] == "port"
+    assert cb["value"] > 0 and abs(cb["value"] * cb["s_per_hologram"] - 1) < 1e-9
+    assert cb["host_cpus"] == os.cpu_count() and "configs[0]" in cb["sample"]

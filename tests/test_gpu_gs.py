@@ -205,3 +205,29 @@ def test_gs_dropin_contract(gpu, golden_dir, capsys):
     assert abs(exp.max() - 255.0) < 1e-9  # expected_outcome *= norm / max
     with pytest.raises(UnboundLocalError):
         gerchberg_saxton(t, args_ns(max_loops=0))
+
+
+@pytest.mark.gpu
+def test_gs_bright_incoming_single_trap_statistics_finite(gpu):
+    """A single-trap target under a very bright incoming amplitude (a_in = 1e6,
+    an intensity image of 1e12): after one iteration the far field holds its
+    energy in one pixel, E = |C|^2 ~ (holo a_in)^2 ~ 4e21 and E^2 ~ 2e43 --
+    beyond float32. The column pass sums E^2 scaled by a power of two ~
+    1/holo^2 (ColParams::stat_k), so the error curve stays finite and equal to
+    the float64 restatement of src/algorithms.py:36-38."""
+    n, loops = 256, 4
+    t = np.zeros((n, n), np.float32)
+    t[37, 101] = 255.0
+    intensity = np.full((n, n), 1e12, np.float32)
+    phi0 = np.random.default_rng(5).uniform(-np.pi, np.pi, (n, n)).astype(np.float32)
+    with gpu.Plan(gpu.ALGO_GS, 1, n, n, gpu.TGT_F32, True, loops) as p:
+        p.set_target(t[None])
+        p.set_ain(np.sqrt(intensity).astype(np.float32))
+        p.set_phase(phi0[None])
+        p.run(loops)
+        ph, e, stats, _ = p.read()
+    err = stats[0, :loops, 3]
+    assert np.isfinite(stats[0, :loops]).all() and np.isfinite(ph).all() and np.isfinite(e).all()
+    _, _, ref_err = orc.gerchberg_saxton_faithful(t, loops, incoming_intensity=intensity, initial_phase=phi0)
+    print(f"[overflow] single trap, a_in 1e6: errors {err} vs float64 {np.asarray(ref_err)}")
+    np.testing.assert_allclose(err, ref_err, rtol=1e-4)

@@ -51,15 +51,19 @@ def test_reference_goldens_both_precisions(gpu, golden_dir, name, prec):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,span,u8", [(1024, 200, True), (1024, 200, False), (2048, 100, False)])
-def test_warm_start_parity_large(gpu, n, span, u8):
+@pytest.mark.parametrize("n,span,u8,seed", [(1024, 200, True, 1024), (1024, 200, False, 1024),
+                                            (1024, 200, False, 1234), (1024, 200, False, 1235),
+                                            (2048, 100, False, 2048)])
+def test_warm_start_parity_large(gpu, n, span, u8, seed):
     """(1024, 200, float32 target) is the bench headline itself (BASELINE.json
-    configs[1]): its plan must be the one bench.py times -- narrow 1024 plan
-    (key 11) on both axes, 2-column tiles, the narrow layout pair (8-wide X,
-    2-wide Y panels), i.e. col_kernel<11, 2, GS_MAIN, f32 target, f32, narrow>
-    -- on the wave-shuffle transform pair (fft_shuffle.hpp) in both kernels,
-    so the gate covers the exact instantiation the roofline is quoted on."""
-    rng = np.random.default_rng(n)
+    configs[1]), gated on three targets: default_rng(1024) and the bench's own
+    first two targets (bench.targets: default_rng(1234 + b), b = 0, 1). Its
+    plan must be the one bench.py times -- narrow 1024 plan (key 11) on both
+    axes, 2-column tiles, the narrow layout pair (8-wide X, 2-wide Y panels),
+    i.e. col_kernel<11, 2, GS_MAIN, f32 target, f32, narrow> -- on the
+    wave-shuffle transform pair (fft_shuffle.hpp) in both kernels, so the gate
+    covers the exact instantiation the roofline is quoted on."""
+    rng = np.random.default_rng(seed)
     t = rng.integers(0, 256, (n, n)).astype(np.uint8) if u8 else rng.uniform(0, 255, (n, n)).astype(np.float32)
     with sfft.set_workers(WORKERS):
         phi_w, _, _ = orc.gerchberg_saxton_faithful(t, 30)
@@ -72,6 +76,7 @@ def test_warm_start_parity_large(gpu, n, span, u8):
     for prec, precision in (("f64", gpu.PRECISION_F64), ("f32", gpu.PRECISION_F32)):
         ph, err = _gpu_warm_run(gpu, t, phi_w, span, precision)
         rms = orc.phase_rms(ph, ref)
-        print(f"[parity] {n}^2 {'u8' if u8 else 'f32'} target, {prec}: warm-start 30+{span}: phase rms {rms:.3e}")
+        print(f"[parity] {n}^2 {'u8' if u8 else 'f32'} target (seed {seed}), {prec}: warm-start 30+{span}: "
+              f"phase rms {rms:.3e}")
         assert rms < PHASE_RMS_TOL
         np.testing.assert_allclose(err, ref_err, rtol=1e-4)
