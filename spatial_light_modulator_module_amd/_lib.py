@@ -101,6 +101,7 @@ _SIGNATURES = [
     ("slm_quantize", _c_int, [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_double, _c_int, _vp]),
     ("slm_transform_hologram", _c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp]),
     ("slm_fft2_intensity", _c_int, [_vp, _c_int, _c_int, _c_int, _vp]),
+    ("slm_fft2_c128", _c_int, [_vp, _vp, _c_int, _c_int, _c_int, _c_int]),
 ]
 
 TRANSFORM_DEFLECT = 1
@@ -345,11 +346,12 @@ class Plan:
     def engine(self) -> tuple[str, str]:
         """(column, row) transform engine of the GS iteration kernels:
         "stockham", "shuffle" (wave-shuffle pair, fft_shuffle.hpp) or, for
-        sides without a radix plan, "dft-gemm" (float64 DFT matrices on
-        rocBLAS ZGEMM, generic.hip)."""
+        sides without a float32 radix plan, "mixed-radix" (float64 radix
+        2..13 kernels, mixed_radix.hpp) or "dft-gemm" (float64 DFT matrices
+        on rocBLAS ZGEMM, generic.hip: sides with a larger prime factor)."""
         c, r = ctypes.c_int(), ctypes.c_int()
         check(self._lib.slm_plan_engine(self.handle, ctypes.byref(c), ctypes.byref(r)), "slm_plan_engine")
-        names = ("stockham", "shuffle", "dft-gemm")
+        names = ("stockham", "shuffle", "dft-gemm", "mixed-radix")
         return names[c.value], names[r.value]
 
     def layout(self) -> tuple[int, int]:
@@ -396,6 +398,20 @@ def fft2(x: np.ndarray, inverse: bool = False) -> np.ndarray:
     out = np.empty_like(a)
     check(load().slm_fft2(ptr(a.view(np.float32)), ptr(out.view(np.float32)), b, h, w, int(bool(inverse))),
           "slm_fft2")
+    return out
+
+
+def fft2_c128(x: np.ndarray, inverse: bool = False) -> np.ndarray:
+    """Unscaled 2-D C2C transform of [..., H, W] complex128 in float64 on the
+    GPU (slm_fft2_c128: the any-size engine's transforms, any shape)."""
+    init()
+    a = np.ascontiguousarray(x, dtype=np.complex128)
+    shape = a.shape
+    h, w = shape[-2:]
+    b = int(np.prod(shape[:-2])) if len(shape) > 2 else 1
+    out = np.empty_like(a)
+    check(load().slm_fft2_c128(ptr(a.view(np.float64)), ptr(out.view(np.float64)), b, h, w, int(bool(inverse))),
+          "slm_fft2_c128")
     return out
 
 

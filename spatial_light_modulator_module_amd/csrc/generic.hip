@@ -1,9 +1,19 @@
-// Any-size engine (generic.hpp): GS / GD iterations whose 2-D transforms are
-// complex float64 products with the DFT matrices, on rocBLAS ZGEMM.
+// Any-size engine (generic.hpp): GS / GD iterations on image sides that no
+// float32 radix plan covers, in complex float64 like the reference's loop.
 //
-// Row-major [H][W] images are, to a column-major BLAS, W x H matrices M^T
-// (leading dimension W). With the symmetric DFT matrices F_N[j][k] =
-// exp(-2 pi i jk / N):
+// Two transform back ends:
+//  * mixed radix (mixed_radix.hpp, mr_inst.hip; the default wherever both
+//    sides factor into 2, 3, 5, 7, 11, 13 and fit a workgroup's LDS): the
+//    iteration is two fused launches -- column pass (forward transform,
+//    projection and statistics, inverse transform) and row pass (inverse,
+//    projection, forward) -- O(N log N), hand-written kernels only;
+//  * DFT-GEMM (any other side, e.g. one with a large prime factor, or
+//    $SLM_GENERIC_ENGINE=gemm): the 2-D transforms as products with the
+//    dense DFT matrices on rocBLAS ZGEMM, O(N^3), with element-wise kernels.
+//
+// DFT-GEMM: row-major [H][W] images are, to a column-major BLAS, W x H
+// matrices M^T (leading dimension W). With the symmetric DFT matrices
+// F_N[j][k] = exp(-2 pi i jk / N):
 //     fft2(M) = F_H M F_W   <=>   fft2(M)^T = F_W M^T F_H
 // so a forward 2-D transform is T = F_W M^T (m = W, n = H, k = W), then
 // T F_H (m = W, n = H, k = H); the inverse (unscaled) takes the conjugate
@@ -20,26 +30,38 @@
 #include <rocblas/rocblas.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <cmath>
 #include <vector>
 
 #include "../../include/slm_hip.h"
 #include "generic.hpp"
 #include "kernels.hpp"
+#include "mixed_radix.hpp"
 
 int slm_set_error(int code, const char* msg);  // slm_capi.hip
 
 namespace slm {
 
 struct GenericEngine {
+    // mixed-radix back end: line plans (twiddles, digit reversal) of both sides
+    bool mr = false;
+    mr::LinePlan pw, ph;     // row (length W) and column (length H) transforms
+    int rpw = 1;             // rows per row tile
+    int cw_log2 = 0;         // columns per column tile = 2^cw_log2
+    int nwg_col = 0;         // column tiles per hologram
+    std::vector<void*> tables;  // device twiddle / reversal tables
+    // DFT-GEMM back end
     rocblas_handle blas = nullptr;
     double2* fh = nullptr;   // F_H [H][H]
     double2* fw = nullptr;   // F_W [W][W] (== fh for square images)
-    double2* a = nullptr;    // GS: A; GD: the inverse-transformed gradient g
-    double2* b = nullptr;    // GS: B, then C in place; GD: u, then F in place
-    double2* d = nullptr;    // GS: D; GD: G
+    // state (row-major complex128 [B][H][W])
+    double2* a = nullptr;    // GEMM GS: A; GD: the inverse-transformed gradient g. Mixed radix: row-pass output
+    double2* b = nullptr;    // GEMM GS: B, then C in place; GD: u, then F in place. Mixed radix: column-pass output
+    double2* d = nullptr;    // GEMM GS: D; GD: G
     double2* x = nullptr;    // GD: the field x
-    double2* tmp = nullptr;  // product intermediate
+    double2* tmp = nullptr;  // GEMM product intermediate
 };
 
 namespace {
@@ -300,13 +322,266 @@ StatsParams stats_of(const GenericView& v, double tol, int iter) {
     return s;
 }
 
+// ------------------------------------------------------------------------
+// mixed-radix back end (host side)
+// ------------------------------------------------------------------------
+// DIF stage radices of a length: 8s (then a 4 or a 2) for the powers of two,
+// then 3, 5, 7, 11, 13; false if another prime divides n or n is too long
+bool mr_radices(int n, std::vector<int>& rad) {
+    rad.clear();
+    if (n < 1 || n > mr::kMaxLine) return false;
+    int t = n, twos = 0;
+    while (t % 2 == 0) {
+        t /= 2;
+        ++twos;
+    }
+    while (twos >= 3 && twos != 4) {
+        rad.push_back(8);
+        twos -= 3;
+    }
+    if (twos == 4) {
+        rad.push_back(4);
+        rad.push_back(4);
+    } else if (twos == 2) {
+        rad.push_back(4);
+    } else if (twos == 1) {
+        rad.push_back(2);
+    }
+    for (int p : {3, 5, 7, 11, 13})
+        while (t % p == 0) {
+            rad.push_back(p);
+            t /= p;
+        }
+    return t == 1 && (int)rad.size() <= mr::kMaxPass;
+}
+
+bool mr_forced_gemm() {
+    const char* e = std::getenv("SLM_GENERIC_ENGINE");
+    return e && !std::strcmp(e, "gemm");
+}
+
+bool mr_shape_ok(int H, int W) {
+    std::vector<int> r;
+    return !mr_forced_gemm() && mr_radices(H, r) && mr_radices(W, r);
+}
+
+// columns per column tile: the widest (<= 16) whose LDS stays within a tile
+int mr_cw_log2(int H, int W) {
+    int c = 0;
+    while (c < 4 && ((long long)H << (c + 1)) <= mr::kTileElems && (1 << (c + 1)) <= W) ++c;
+    return c;
+}
+
+// rows per row tile: as many as a tile holds, halved while the launch would
+// leave the chip short of workgroups and a tile still holds >= 2048 elements
+int mr_rpw(int B, int H, int W) {
+    int r = std::max(1, std::min(H, mr::kTileElems / W));
+    while (r > 1 && (long long)B * ((H + r - 1) / r) < 512 && (long long)(r / 2) * W >= 2048) r /= 2;
+    return r;
+}
+
+// twiddles exp(-2 pi i t / n) and the DIF output order's natural indices
+int mr_plan_line(GenericEngine* g, int n, mr::LinePlan* pl, hipStream_t st) {
+    std::vector<int> rad;
+    if (!mr_radices(n, rad)) return slm_set_error(SLM_ERR_UNSUPPORTED, "mixed radix: unsupported length");
+    pl->n = n;
+    pl->np = (int)rad.size();
+    for (int i = 0; i < pl->np; ++i) pl->radix[i] = rad[i];
+    std::vector<double> tw((size_t)n * 2);
+    for (long long t = 0; t < n; ++t) {
+        const double ang = 2.0 * M_PI * (double)t / (double)n;
+        tw[t * 2] = std::cos(ang);
+        tw[t * 2 + 1] = -std::sin(ang);
+    }
+    std::vector<int> rev(n);
+    for (int e = 0; e < n; ++e) {
+        int k = 0, mul = 1, m = n, rem = e;
+        for (int R : rad) {
+            m /= R;
+            const int q = rem / m;
+            rem -= q * m;
+            k += q * mul;
+            mul *= R;
+        }
+        rev[e] = k;
+    }
+    void *dtw = nullptr, *drev = nullptr;
+    if (hipMalloc(&dtw, tw.size() * sizeof(double)) != hipSuccess) return slm_set_error(SLM_ERR_HIP, "mixed radix: allocation");
+    g->tables.push_back(dtw);
+    if (hipMalloc(&drev, rev.size() * sizeof(int)) != hipSuccess) return slm_set_error(SLM_ERR_HIP, "mixed radix: allocation");
+    g->tables.push_back(drev);
+    G_HIP(hipMemcpyAsync(dtw, tw.data(), tw.size() * sizeof(double), hipMemcpyHostToDevice, st));
+    G_HIP(hipMemcpyAsync(drev, rev.data(), rev.size() * sizeof(int), hipMemcpyHostToDevice, st));
+    G_HIP(hipStreamSynchronize(st));
+    pl->tw = static_cast<const double2*>(dtw);
+    pl->rev = static_cast<const int*>(drev);
+    return 0;
+}
+
+int mr_roots(hipStream_t st) {
+    std::vector<double2> roots((mr::kMaxRadix + 1) * mr::kMaxRadix, make_double2(0.0, 0.0));
+    for (int R = 1; R <= mr::kMaxRadix; ++R)
+        for (int q = 0; q < R; ++q) {
+            const double ang = 2.0 * M_PI * (double)q / (double)R;
+            roots[R * mr::kMaxRadix + q] = make_double2(std::cos(ang), -std::sin(ang));
+        }
+    if (mr::mr_set_roots(roots.data(), st)) return slm_set_error(SLM_ERR_HIP, "mixed radix: root table upload failed");
+    return 0;
+}
+
+// kernel-class marks around a launch (slm_plan_run_timed events)
+struct Mark {
+    const GenericView& v;
+    int cls;
+    Mark(const GenericView& vv, int c) : v(vv), cls(c) {
+        if (v.mark) v.mark(v.mark_ctx, cls, 1);
+    }
+    ~Mark() {
+        if (v.mark) v.mark(v.mark_ctx, cls, 0);
+    }
+};
+
+int mr_row(GenericEngine* g, const GenericView& v, int op, mr::RowArgs a, int cls = SLM_KERNEL_OTHER) {
+    a.pl = g->pw;
+    a.B = v.B;
+    a.H = v.H;
+    a.W = v.W;
+    a.rpw = g->rpw;
+    a.holo = v.holo;
+    a.inv_s = 1.0 / (double)v.holo;
+    a.ain = v.ain;
+    a.stop = v.stop;
+    const int grid = v.B * ((v.H + g->rpw - 1) / g->rpw);
+    const size_t lds = (size_t)g->rpw * v.W * sizeof(double2);
+    Mark mk(v, cls);
+    if (mr::mr_row_launch(op, a, grid, lds, v.stream)) return slm_set_error(SLM_ERR_HIP, "mixed-radix row launch failed");
+    return 0;
+}
+
+int mr_col(GenericEngine* g, const GenericView& v, int op, mr::ColArgs a, int cls = SLM_KERNEL_OTHER) {
+    a.pl = g->ph;
+    a.B = v.B;
+    a.H = v.H;
+    a.W = v.W;
+    a.cw_log2 = g->cw_log2;
+    a.nwg = g->nwg_col;
+    a.holo = v.holo;
+    a.tgt = v.tgt;
+    a.tt = v.tt;
+    a.e_out = v.e_out;
+    a.partials = v.partials;
+    a.stop = v.stop;
+    a.stats = v.stats;
+    a.norm = v.norm;
+    a.max_loops = v.max_loops;
+    const int grid = v.B * g->nwg_col;
+    const size_t lds = ((size_t)v.H << g->cw_log2) * sizeof(double2);
+    Mark mk(v, cls);
+    if (mr::mr_col_launch(op, a, grid, lds, v.stream)) return slm_set_error(SLM_ERR_HIP, "mixed-radix column launch failed");
+    return 0;
+}
+
+// out = fft2 / unscaled ifft2 of in (device complex128 [B][H][W]; in may equal out)
+int mr_fft2(GenericEngine* g, const GenericView& v, const double2* in, double2* out, bool inverse) {
+    mr::RowArgs r;
+    r.in = in;
+    r.out = g->a;
+    if (int rc = mr_row(g, v, inverse ? mr::RO_INV : mr::RO_FWD, r)) return rc;
+    mr::ColArgs c;
+    c.in = g->a;
+    c.out = out;
+    return mr_col(g, v, inverse ? mr::CO_INV : mr::CO_FWD, c);
+}
+
+int mr_enqueue(GenericEngine* g, const GenericView& v, int loops, double tol, int checked, float wa, bool phase_set,
+               bool field_set) {
+    const long long n = (long long)v.B * v.holo;
+    const int grid = grid_of(n);
+    hipStream_t st = v.stream;
+    const double tol_or_none = checked ? tol : -1.0;
+    mr::RowArgs r;
+    mr::ColArgs c;
+    r.checked = c.checked = checked;
+    c.wa = wa;
+    if (v.algo == SLM_ALGO_GS) {
+        // setup (src/algorithms.py:14-27): the warm start B = a_in exp(i phi), or
+        // A0 = ifft2(sqrt T) in complex64, B = a_in A0/|A0|; row-transformed into a
+        if (phase_set) {
+            r.phase_in = v.phase_in;
+            r.out = g->a;
+            if (int rc = mr_row(g, v, mr::RO_WARM, r)) return rc;
+        } else {
+            c.out = g->b;
+            if (int rc = mr_col(g, v, mr::CO_AMP_INV, c)) return rc;
+            r.in = g->b;
+            r.out = g->a;
+            if (int rc = mr_row(g, v, mr::RO_COLD, r)) return rc;
+        }
+        for (int i = 0; i < loops; ++i) {
+            c.in = g->a;
+            c.out = g->b;
+            c.iter = i;
+            c.write_e = (checked || i + 1 == loops) ? 1 : 0;
+            if (int rc = mr_col(g, v, mr::CO_GS, c, SLM_KERNEL_COL_MAIN)) return rc;
+            if (checked) hipLaunchKernelGGL(k_reduce_iter, dim3(v.B), dim3(256), 0, st, stats_of(v, tol_or_none, i));
+            r.in = g->b;
+            r.out = g->a;
+            r.iter = i;
+            r.last = i + 1 == loops;
+            r.phase_out = v.phase_out;
+            if (int rc = mr_row(g, v, mr::RO_GS, r, SLM_KERNEL_ROW_MAIN)) return rc;
+        }
+    } else {
+        // setup (make_initial_guess, src/algorithms.py:115-158): the host field, or
+        // the "fourier" guess a_in exp(i angle(ifft2(sqrt T)))
+        r.x = g->x;
+        if (field_set) {
+            r.field0 = v.field0;
+            r.out = g->a;
+            if (int rc = mr_row(g, v, mr::RO_GD_INIT, r)) return rc;
+        } else {
+            c.out = g->b;
+            if (int rc = mr_col(g, v, mr::CO_AMP_INV, c)) return rc;
+            r.in = g->b;
+            r.out = g->a;
+            if (int rc = mr_row(g, v, mr::RO_GD_FOURIER, r)) return rc;
+        }
+        r.lr = v.lr;
+        for (int i = 0; i < loops; ++i) {
+            c.in = g->a;
+            c.iter = i;
+            c.write_e = (checked || i + 1 == loops) ? 1 : 0;
+            if (int rc = mr_col(g, v, mr::CO_GD_STATS, c, SLM_KERNEL_GD_STATS)) return rc;
+            // this iteration's max |F|^2 (and, checked, its error against the tolerance)
+            hipLaunchKernelGGL(k_reduce_iter, dim3(v.B), dim3(256), 0, st, stats_of(v, tol_or_none, i));
+            c.out = g->b;
+            if (int rc = mr_col(g, v, mr::CO_GD_GRAD, c, SLM_KERNEL_COL_MAIN)) return rc;
+            r.in = g->b;
+            r.out = g->a;
+            r.iter = i;
+            r.last = i + 1 == loops;
+            if (int rc = mr_row(g, v, mr::RO_GD, r, SLM_KERNEL_ROW_MAIN)) return rc;
+        }
+        hipLaunchKernelGGL(k_phase, dim3(grid), dim3(kGT), 0, st, g->x, v.phase_out, n);
+    }
+    G_HIP(hipGetLastError());
+    return 0;
+}
+
 }  // namespace
 
-int generic_nwg(long long holo) { return (int)std::max<long long>(1, std::min<long long>(1024, holo / (kGT * 8))); }
+int generic_nwg(int H, int W, long long holo) {
+    if (mr_shape_ok(H, W)) return (W + (1 << mr_cw_log2(H, W)) - 1) >> mr_cw_log2(H, W);
+    return (int)std::max<long long>(1, std::min<long long>(1024, holo / (kGT * 8)));
+}
+
+bool generic_uses_blas(const GenericEngine* g) { return g && !g->mr; }
 
 void generic_destroy(GenericEngine* g) {
     if (!g) return;
     for (void* p : {(void*)g->a, (void*)g->b, (void*)g->d, (void*)g->x, (void*)g->tmp, (void*)g->fw})
+        if (p) (void)hipFree(p);
+    for (void* p : g->tables)
         if (p) (void)hipFree(p);
     if (g->fh && g->fh != g->fw) (void)hipFree(g->fh);
     if (g->blas) (void)rocblas_destroy_handle(g->blas);
@@ -324,6 +599,23 @@ int generic_create(const GenericView& v, GenericEngine** out) {
     auto alloc = [&](double2** p, size_t count) {
         return hipMalloc((void**)p, count * sizeof(double2)) == hipSuccess;
     };
+    if (mr_shape_ok(v.H, v.W)) {  // mixed radix: two state buffers (+ the GD field), line plans
+        g->mr = true;
+        g->cw_log2 = mr_cw_log2(v.H, v.W);
+        g->nwg_col = (v.W + (1 << g->cw_log2) - 1) >> g->cw_log2;
+        g->rpw = mr_rpw(v.B, v.H, v.W);
+        if (g->nwg_col != v.nwg) return fail_free(slm_set_error(SLM_ERR_STATE, "mixed radix: partial-slab mismatch"));
+        if (!alloc(&g->a, n) || !alloc(&g->b, n) || (v.algo == SLM_ALGO_GD && !alloc(&g->x, n)))
+            return fail_free(slm_set_error(SLM_ERR_HIP, "mixed radix: device allocation failed"));
+        if (int rc = mr_plan_line(g, v.W, &g->pw, v.stream)) return fail_free(rc);
+        if (int rc = mr_plan_line(g, v.H, &g->ph, v.stream)) return fail_free(rc);
+        if (int rc = mr_roots(v.stream)) return fail_free(rc);
+        // the state is defined before any run (read_field of a fresh plan is refused upstream)
+        if (hipMemsetAsync(g->a, 0, n * sizeof(double2), v.stream) != hipSuccess)
+            return fail_free(slm_set_error(SLM_ERR_HIP, "mixed radix: state initialisation failed"));
+        *out = g;
+        return 0;
+    }
     if (!alloc(&g->a, n) || !alloc(&g->b, n) || !alloc(&g->d, n) || !alloc(&g->tmp, n) ||
         (v.algo == SLM_ALGO_GD && !alloc(&g->x, n)) || !alloc(&g->fw, (size_t)v.W * v.W))
         return fail_free(slm_set_error(SLM_ERR_HIP, "DFT engine: device allocation failed"));
@@ -354,6 +646,7 @@ int generic_create(const GenericView& v, GenericEngine** out) {
 
 int generic_enqueue(GenericEngine* g, const GenericView& v, int loops, double tol, int checked, float wa,
                     bool phase_set, bool field_set) {
+    if (g->mr) return mr_enqueue(g, v, loops, tol, checked, wa, phase_set, field_set);
     const long long n = (long long)v.B * v.holo;
     const int grid = grid_of(n);
     const dim3 sgrid(v.nwg, v.B);
@@ -417,7 +710,7 @@ int generic_field(GenericEngine* g, const GenericView& v, float2* out) {
 int generic_fft2(GenericEngine* g, const GenericView& v, const float2* in, float2* out, int inverse) {
     const long long n = (long long)v.B * v.holo;
     hipLaunchKernelGGL(k_c64_to_c128, dim3(grid_of(n)), dim3(kGT), 0, v.stream, in, g->b, n);
-    if (int rc = dft2(g, v, g->b, g->b, inverse != 0)) return rc;
+    if (int rc = g->mr ? mr_fft2(g, v, g->b, g->b, inverse != 0) : dft2(g, v, g->b, g->b, inverse != 0)) return rc;
     hipLaunchKernelGGL(k_c128_to_c64, dim3(grid_of(n)), dim3(kGT), 0, v.stream, g->b, out, n);
     G_HIP(hipGetLastError());
     return 0;
@@ -426,10 +719,14 @@ int generic_fft2(GenericEngine* g, const GenericView& v, const float2* in, float
 int generic_intensity(GenericEngine* g, const GenericView& v, const float* phase, float* out) {
     const long long n = (long long)v.B * v.holo;
     hipLaunchKernelGGL(k_phase_exp, dim3(grid_of(n)), dim3(kGT), 0, v.stream, phase, g->b, n);
-    if (int rc = dft2(g, v, g->b, g->b, false)) return rc;
+    if (int rc = g->mr ? mr_fft2(g, v, g->b, g->b, false) : dft2(g, v, g->b, g->b, false)) return rc;
     hipLaunchKernelGGL(k_abs2, dim3(grid_of(n)), dim3(kGT), 0, v.stream, g->b, out, n);
     G_HIP(hipGetLastError());
     return 0;
+}
+
+int generic_fft2_z(GenericEngine* g, const GenericView& v, const double2* in, double2* out, int inverse) {
+    return g->mr ? mr_fft2(g, v, in, out, inverse != 0) : dft2(g, v, in, out, inverse != 0);
 }
 
 }  // namespace slm

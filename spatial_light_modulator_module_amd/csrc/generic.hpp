@@ -1,11 +1,11 @@
-// Any-size engine of the GS / GD loops: image sides that no radix plan
+// Any-size engine of the GS / GD loops: image sides that no float32 radix plan
 // (plans.hpp) covers. The reference takes any (h, w) (src/algorithms.py:20-27;
-// scipy.fft handles every length), so such plans run their 2-D transforms as
-// complex float64 matrix products with the DFT matrices (rocBLAS ZGEMM on the
-// MI355X matrix cores) and the projections / statistics / GD update as
-// element-wise kernels, all state complex128 in HBM, row-major. slm_capi.hip
-// owns the plan's buffers; this engine owns its work buffers, the DFT matrices
-// and the rocBLAS handle.
+// scipy.fft handles every length), so such plans run in complex float64 with
+// row-major state: on hand-written mixed-radix transforms (mixed_radix.hpp)
+// where both sides factor into 2, 3, 5, 7, 11, 13, otherwise as products with
+// the dense DFT matrices (rocBLAS ZGEMM on the MI355X matrix cores) plus
+// element-wise kernels. slm_capi.hip owns the plan's buffers; this engine owns
+// its work buffers, line plans / DFT matrices and the rocBLAS handle.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -30,10 +30,17 @@ struct GenericView {
     int* stop = nullptr;              // [B]
     const double* norm = nullptr;     // max(T) [B]
     const double* sum_t2 = nullptr;   // sum T^2 [B]
+    // optional kernel-class marks around each iteration launch (timed runs):
+    // mark(ctx, class, 1) before, mark(ctx, class, 0) after
+    int (*mark)(void* ctx, int cls, int begin) = nullptr;
+    void* mark_ctx = nullptr;
 };
 
-// statistics blocks per hologram (the partials' nwg)
-int generic_nwg(long long holo);
+// statistics blocks per hologram (the partials' nwg): column tiles of the
+// mixed-radix back end, element chunks of the DFT-GEMM one
+int generic_nwg(int H, int W, long long holo);
+// true for the DFT-GEMM back end (rocBLAS calls: runs are not graph-captured)
+bool generic_uses_blas(const GenericEngine* g);
 int generic_create(const GenericView& v, GenericEngine** out);
 void generic_destroy(GenericEngine* g);
 // one full run (setup, loops iterations, phase and expected output, statistics),
@@ -44,6 +51,8 @@ int generic_enqueue(GenericEngine* g, const GenericView& v, int loops, double to
 int generic_field(GenericEngine* g, const GenericView& v, float2* out);
 // unscaled 2-D DFT of complex64 [B][H][W] (device in / out; in may equal out)
 int generic_fft2(GenericEngine* g, const GenericView& v, const float2* in, float2* out, int inverse);
+// unscaled 2-D DFT of complex128 [B][H][W] (device in / out; in may equal out)
+int generic_fft2_z(GenericEngine* g, const GenericView& v, const double2* in, double2* out, int inverse);
 // |fft2(exp(i phase))|^2, float32 [B][H][W] (device)
 int generic_intensity(GenericEngine* g, const GenericView& v, const float* phase, float* out);
 

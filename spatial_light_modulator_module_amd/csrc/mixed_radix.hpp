@@ -1,0 +1,320 @@
+// Mixed-radix float64 transforms for image sides without a float32 radix plan
+// (plans.hpp covers 2^k and 768): any side whose prime factors are <= 13 and
+// that fits one workgroup's LDS, e.g. the 1080 x 1920 and 1280 x 1024 SLM
+// panels. The reference transforms every length in O(N log N) through
+// pocketfft (src/algorithms.py:27,31,34; scipy.fft); these kernels do the same
+// on the device, in complex128 like the reference's loop, so the any-shape
+// engine (generic.hip) no longer multiplies by dense DFT matrices there.
+//
+// One line = one 1-D transform held in LDS (complex128), transformed in place
+// one radix pass at a time, one butterfly in registers at a time (no staging
+// of a thread's whole share: registers stay far below the 128 that two
+// 512-thread workgroups per CU allow). Stages R_0, R_1, ... of span L (L = n
+// first, then L / R_0, ...), m = L / R, block start b0 (a multiple of L), j < m:
+//   DIF (natural in, digit-reversed out):
+//     y = DFT_R(x[b0 + j + r m], r < R);  x[b0 + j + q m] = y_q w_L^(q j)
+//   DIT (digit-reversed in, natural out): the adjoint, stages in reverse order
+//     u_q = x[b0 + j + q m] w_L^(q j);  x[b0 + j + r m] = DFT_R(u)_r
+// (w conjugated, DFT_R conjugated for the inverse). After a DIF the element at
+// position e is frequency rev[e] = q_0 + R_0 q_1 + R_0 R_1 q_2 + ..., where
+// e = q_0 (n / R_0) + q_1 (n / (R_0 R_1)) + ... (checked against numpy.fft).
+// The GS / GD projections between a launch's two transforms are element-wise,
+// so they run on the digit-reversed order (reading the target / a_in and
+// writing phases / the expected output at the natural index rev[e]), and the
+// pair DIF -> projection -> DIT never permutes. A lone transform (setup,
+// fft2 helpers) loads its input gathered in digit-reversed order and runs the
+// DIT.
+//
+// A workgroup holds several lines: consecutive rows of a row tile (element
+// stride 1), or the columns of a column tile interleaved ([h][c], element
+// stride CW, butterflies enumerated column-fastest so neighbouring lanes touch
+// neighbouring LDS words).
+//
+// The GS / GD iteration is two launches (plus the GD statistics split), as in
+// the float32 engine (kernels.hpp): the column launch runs forward transform
+// -> projection and statistics -> inverse transform, the row launch inverse ->
+// projection -> forward, so each launch reads and writes the field once.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernels.hpp"
+
+namespace slm {
+namespace mr {
+
+constexpr int kThreads = 512;  // threads per workgroup of every mixed-radix kernel
+constexpr int kMaxPass = 16;
+constexpr int kMaxRadix = 13;
+// LDS of one tile: at most this many complex128 elements (72 KiB: two
+// workgroups per CU); a single line may take up to kMaxLine (one per CU)
+constexpr int kTileElems = 4608;
+constexpr int kMaxLine = 8192;
+
+// one line length's plan: radices in DIF stage order, the twiddle table
+// tw[t] = exp(-2 pi i t / n), t < n (host-computed in double), and the
+// digit reversal rev[e] of the DIF output order
+struct LinePlan {
+    int n = 1;
+    int np = 0;
+    int radix[kMaxPass] = {};
+    const double2* tw = nullptr;
+    const int* rev = nullptr;
+};
+
+// roots of the small DFTs: kRoots[R][q] = exp(-2 pi i q / R) (copied per device
+// and per translation unit by mr_set_roots; wave-uniform indices -> scalar loads)
+namespace {
+__constant__ double2 kRoots[kMaxRadix + 1][kMaxRadix];
+}
+
+__device__ __forceinline__ double2 cadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double2 csub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+    return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ double2 cmulc(double2 a, double2 b) {  // a * conj(b)
+    return make_double2(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
+}
+// i sigma z, sigma = -1 forward, +1 inverse
+template <bool INV>
+__device__ __forceinline__ double2 isg(double2 z) {
+    return INV ? make_double2(-z.y, z.x) : make_double2(z.y, -z.x);
+}
+
+template <int R, bool INV>
+struct Dft;
+template <bool INV>
+struct Dft<2, INV> {
+    __device__ __forceinline__ static void run(double2 (&u)[2]) {
+        const double2 a = u[0];
+        u[0] = cadd(a, u[1]);
+        u[1] = csub(a, u[1]);
+    }
+};
+template <bool INV>
+struct Dft<4, INV> {
+    __device__ __forceinline__ static void run(double2 (&u)[4]) {
+        const double2 a = cadd(u[0], u[2]), b = csub(u[0], u[2]);
+        const double2 c = cadd(u[1], u[3]), d = isg<INV>(csub(u[1], u[3]));
+        u[0] = cadd(a, c);
+        u[2] = csub(a, c);
+        u[1] = cadd(b, d);
+        u[3] = csub(b, d);
+    }
+};
+template <bool INV>
+struct Dft<8, INV> {
+    __device__ __forceinline__ static void run(double2 (&u)[8]) {
+        double2 e[4] = {u[0], u[2], u[4], u[6]}, o[4] = {u[1], u[3], u[5], u[7]};
+        Dft<4, INV>::run(e);
+        Dft<4, INV>::run(o);
+        constexpr double h = 0.70710678118654752440;  // sqrt(1/2)
+        constexpr double s = INV ? 1.0 : -1.0;
+        // o_q *= w8^q, w8 = exp(sigma 2 pi i / 8)
+        o[1] = make_double2(h * (o[1].x - s * o[1].y), h * (o[1].y + s * o[1].x));
+        o[2] = isg<INV>(o[2]);
+        o[3] = make_double2(h * (-o[3].x - s * o[3].y), h * (-o[3].y + s * o[3].x));
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            u[q] = cadd(e[q], o[q]);
+            u[q + 4] = csub(e[q], o[q]);
+        }
+    }
+};
+// odd R: y_q = u_0 + sum_s a_s cos(2 pi s q / R) + i sigma sum_s b_s sin(2 pi s q / R),
+// a_s = u_s + u_(R-s), b_s = u_s - u_(R-s); y_(R-q) the conjugate combination
+template <int R, bool INV>
+struct Dft {
+    static_assert(R % 2 == 1 && R <= kMaxRadix, "odd radices up to kMaxRadix");
+    __device__ __forceinline__ static void run(double2 (&u)[R]) {
+        constexpr int H = R / 2;
+        double2 a[H], b[H];
+        double2 y0 = u[0];
+#pragma unroll
+        for (int s = 1; s <= H; ++s) {
+            a[s - 1] = cadd(u[s], u[R - s]);
+            b[s - 1] = csub(u[s], u[R - s]);
+            y0 = cadd(y0, a[s - 1]);
+        }
+#pragma unroll
+        for (int q = 1; q <= H; ++q) {
+            double2 A = u[0], Bv = make_double2(0.0, 0.0);
+#pragma unroll
+            for (int s = 1; s <= H; ++s) {
+                const double2 w = kRoots[R][(s * q) % R];  // (cos, -sin)
+                A.x = fma(a[s - 1].x, w.x, A.x);
+                A.y = fma(a[s - 1].y, w.x, A.y);
+                Bv.x = fma(b[s - 1].x, -w.y, Bv.x);
+                Bv.y = fma(b[s - 1].y, -w.y, Bv.y);
+            }
+            const double2 j = isg<INV>(Bv);
+            u[q] = cadd(A, j);
+            u[R - q] = csub(A, j);
+        }
+        u[0] = y0;
+    }
+};
+
+// Geometry of the lines in one workgroup's LDS: line l, element e at
+// lds[l * ls + e * es]. LINEFAST: butterflies enumerated line-fastest (column
+// tiles) instead of element-fastest (row tiles).
+struct Lines {
+    int count, ls, es;
+};
+
+template <bool LINEFAST>
+__device__ __forceinline__ int bf_base(const Lines& g, int gi, int per_line, int L, int m, int& j) {
+    int line, bf;
+    if (LINEFAST) {
+        line = gi % g.count;
+        bf = gi / g.count;
+    } else {
+        line = gi / per_line;
+        bf = gi - line * per_line;
+    }
+    const int blk = bf / m;
+    j = bf - blk * m;
+    return line * g.ls + (blk * L + j) * g.es;
+}
+
+// one in-place pass of radix R and span L over every line of the tile
+template <int R, bool INV, bool LINEFAST, bool DIT>
+__device__ __forceinline__ void pass(double2* lds, const Lines& g, int n, int L, const double2* __restrict__ tw) {
+    const int m = L / R;
+    const int per_line = n / R;
+    const int nb = g.count * per_line;
+    const int tstride = n / L;
+    const int step = m * g.es;
+    for (int gi = threadIdx.x; gi < nb; gi += kThreads) {
+        int j;
+        const int base = bf_base<LINEFAST>(g, gi, per_line, L, m, j);
+        double2 u[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) u[r] = lds[base + r * step];
+        if (DIT) {
+#pragma unroll
+            for (int q = 1; q < R; ++q) {
+                const double2 w = tw[q * j * tstride];
+                u[q] = INV ? cmulc(u[q], w) : cmul(u[q], w);
+            }
+        }
+        Dft<R, INV>::run(u);
+        if (!DIT) {
+#pragma unroll
+            for (int q = 1; q < R; ++q) {
+                const double2 w = tw[q * j * tstride];
+                u[q] = INV ? cmulc(u[q], w) : cmul(u[q], w);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) lds[base + r * step] = u[r];
+    }
+    __syncthreads();
+}
+
+template <bool INV, bool LINEFAST, bool DIT>
+__device__ __forceinline__ void pass_r(int R, double2* lds, const Lines& g, int n, int L, const double2* tw) {
+    switch (R) {
+        case 2: pass<2, INV, LINEFAST, DIT>(lds, g, n, L, tw); break;
+        case 3: pass<3, INV, LINEFAST, DIT>(lds, g, n, L, tw); break;
+        case 4: pass<4, INV, LINEFAST, DIT>(lds, g, n, L, tw); break;
+        case 5: pass<5, INV, LINEFAST, DIT>(lds, g, n, L, tw); break;
+        case 7: pass<7, INV, LINEFAST, DIT>(lds, g, n, L, tw); break;
+        case 8: pass<8, INV, LINEFAST, DIT>(lds, g, n, L, tw); break;
+        case 11: pass<11, INV, LINEFAST, DIT>(lds, g, n, L, tw); break;
+        default: pass<13, INV, LINEFAST, DIT>(lds, g, n, L, tw); break;
+    }
+}
+
+// natural order in -> digit-reversed (rev) order out, every line of the tile
+template <bool INV, bool LINEFAST>
+__device__ __forceinline__ void fft_dif(double2* lds, const Lines& g, const LinePlan& pl) {
+    int L = pl.n;
+    for (int s = 0; s < pl.np; ++s) {
+        const int R = pl.radix[s];
+        pass_r<INV, LINEFAST, false>(R, lds, g, pl.n, L, pl.tw);
+        L /= R;
+    }
+}
+// digit-reversed order in -> natural order out
+template <bool INV, bool LINEFAST>
+__device__ __forceinline__ void fft_dit(double2* lds, const Lines& g, const LinePlan& pl) {
+    int L = 1;
+    for (int s = pl.np - 1; s >= 0; --s) {
+        const int R = pl.radix[s];
+        L *= R;
+        pass_r<INV, LINEFAST, true>(R, lds, g, pl.n, L, pl.tw);
+    }
+}
+
+// ------------------------------------------------------------------------
+// kernels
+// ------------------------------------------------------------------------
+enum RowOp : int {
+    RO_FWD = 0,        // in -> fwd -> out
+    RO_INV = 1,        // in -> inv -> out
+    RO_COLD = 2,       // GS cold start: in (column-inverse of a_T) -> inv -> A0 rounded to complex64
+                       //   (src/algorithms.py:27) -> B = a_in A0/|A0| -> fwd -> out
+    RO_WARM = 3,       // GS warm start: B = a_in exp(i phi) (complex64 exp, as numpy) -> fwd -> out
+    RO_GS = 4,         // GS: in -> inv -> A; last (or stopped): phase = angle(A) (:48), else
+                       //   B = a_in A/|A| (:30) -> fwd -> out
+    RO_GD_FOURIER = 5, // GD "fourier" guess: in -> inv -> complex64 -> x = a_in exp(i angle) (:153-156)
+                       //   -> u = a_in x/|x| (:84) -> fwd -> out
+    RO_GD_INIT = 6,    // GD host field: x = field0 (complex64) -> u -> fwd -> out
+    RO_GD = 7,         // GD: in (column-inverse of G) -> inv -> g a_in / S; dEdX_complex, x -= lr dEdX
+                       //   (:87-91, :179-185) -> u -> fwd -> out
+    RO_NUM = 8
+};
+enum ColOp : int {
+    CO_FWD = 0,       // in -> fwd -> out
+    CO_INV = 1,       // in -> inv -> out
+    CO_AMP_INV = 2,   // a_T = sqrt(T) as numpy forms it -> inv -> out
+    CO_GS = 3,        // in -> fwd -> C; E = |C|^2 statistics, expected output, D = a_T C/|C| (:33,36-38)
+                      //   -> inv -> out
+    CO_GD_STATS = 4,  // in -> fwd -> F; statistics of P = |F|^2 (:85-86), output
+    CO_GD_GRAD = 5,   // in -> fwd -> G = mask F (s P - T) (:80,85-88) -> inv -> out
+    CO_NUM = 6
+};
+
+struct RowArgs {
+    const double2* in = nullptr;
+    double2* out = nullptr;
+    const float* ain = nullptr;        // [H][W] or nullptr (uniform)
+    const float* phase_in = nullptr;   // RO_WARM
+    float* phase_out = nullptr;        // RO_GS
+    double2* x = nullptr;              // GD state
+    const float2* field0 = nullptr;    // RO_GD_INIT
+    const float* lr = nullptr;         // RO_GD, per iteration
+    const int* stop = nullptr;         // [B]
+    int iter = 0, checked = 0, last = 0;
+    int B = 0, H = 0, W = 0, rpw = 1;  // rows per workgroup
+    long long holo = 0;
+    double inv_s = 0.0;
+    LinePlan pl;                       // length W
+};
+struct ColArgs {
+    const double2* in = nullptr;
+    double2* out = nullptr;
+    const void* tgt = nullptr;
+    int tt = 0;                        // TGT_U8 / TGT_F32 (row-major, as uploaded)
+    float* e_out = nullptr;
+    double* partials = nullptr;        // [B][max_loops][nwg][4]
+    const int* stop = nullptr;
+    const double* stats = nullptr;     // CO_GD_GRAD: this iteration's max |F|^2
+    const double* norm = nullptr;
+    int iter = 0, checked = 0, write_e = 0, max_loops = 1;
+    int nwg = 1, cw_log2 = 0, B = 0, H = 0, W = 0;
+    float wa = 0.f;
+    long long holo = 0;
+    LinePlan pl;                       // length H
+};
+
+// host launchers (mr_inst.hip; lds = tile elements x 16 B; 0 or -1 on a launch error)
+int mr_row_launch(int op, const RowArgs& a, int grid, size_t lds, hipStream_t st);
+int mr_col_launch(int op, const ColArgs& a, int grid, size_t lds, hipStream_t st);
+// small-DFT roots (host table [kMaxRadix + 1][kMaxRadix]) into the current device's copy
+int mr_set_roots(const double2* roots, hipStream_t st);
+
+}  // namespace mr
+}  // namespace slm

@@ -1,0 +1,284 @@
+// Mixed-radix float64 iteration kernels (mixed_radix.hpp).
+//
+// Row tile: `rpw` consecutive rows of one hologram (one contiguous run of
+// rpw * W complex128 in HBM). Column tile: 2^cw_log2 adjacent columns of one
+// hologram, all H rows, held [h][c] in LDS (each row's 2^cw_log2 * 16 B piece
+// is one contiguous segment in HBM). Element-wise work mirrors the DFT-GEMM
+// engine's kernels in generic.hip (same formulas, same numpy dtype rules), so
+// the two engines differ only in how the transforms round.
+//
+// Order inside a launch: the first transform is a DIF (natural in, digit-
+// reversed out), the projection works on the digit-reversed order with
+// natural indices rev[e], the second transform is a DIT (natural out). Lone
+// transforms gather their input in digit-reversed order and run a DIT.
+#include <hip/hip_runtime.h>
+
+#include "mixed_radix.hpp"
+
+namespace slm {
+namespace mr {
+namespace {
+
+// waves per SIMD the register budget must allow: 4 = two 512-thread
+// workgroups per CU (<= 128 VGPRs), which their LDS (<= 72 KiB each) allows
+#ifndef MR_WPE
+#define MR_WPE 4
+#endif
+
+__device__ __forceinline__ double amp_of(const void* tgt, int tt, long long i) {
+    if (tt == TGT_U8) return (double)TgtLoad<TGT_U8>::amp(TgtLoad<TGT_U8>::load(tgt, i));
+    return (double)(float)sqrt((double)static_cast<const float*>(tgt)[i]);  // numpy: sqrt(float32) is float32
+}
+__device__ __forceinline__ double t_of(const void* tgt, int tt, long long i) {
+    return tt == TGT_U8 ? (double)static_cast<const uint8_t*>(tgt)[i] : (double)static_cast<const float*>(tgt)[i];
+}
+// a exp(i angle(z)) == a z / |z|, angle(0) = 0 -> a (src/algorithms.py:30,33)
+__device__ __forceinline__ double2 unit_of(double2 z, double a) {
+    const double n2 = z.x * z.x + z.y * z.y;
+    if (n2 == 0.0) return make_double2(a, 0.0);
+    const double r = a / sqrt(n2);
+    return make_double2(z.x * r, z.y * r);
+}
+// x / |x| a (src/algorithms.py:84; |x| = 0 gives NaN as there)
+__device__ __forceinline__ double2 u_of(double2 x, double a) {
+    const double r = a / sqrt(x.x * x.x + x.y * x.y);
+    return make_double2(x.x * r, x.y * r);
+}
+__device__ __forceinline__ double2 round_c64(double2 z) { return make_double2((double)(float)z.x, (double)(float)z.y); }
+
+template <int OP>
+__global__ void __launch_bounds__(kThreads, MR_WPE) mr_row_kernel(RowArgs a) {
+    extern __shared__ double2 lds[];
+    const int tiles = (a.H + a.rpw - 1) / a.rpw;
+    const int b = blockIdx.x / tiles;
+    const int row0 = (blockIdx.x - b * tiles) * a.rpw;
+    const int rows = min(a.rpw, a.H - row0);
+    const int W = a.W;
+    const int ne = rows * W;
+    const long long pix0 = (long long)row0 * W;  // within the hologram
+    const long long off = (long long)b * a.holo + pix0;
+    const int* __restrict__ rev = a.pl.rev;
+    if constexpr (OP == RO_GS || OP == RO_GD) {
+        if (a.checked && a.iter > a.stop[b]) return;  // stopped earlier: frozen (src/algorithms.py:29,83)
+    }
+    // position e of the tile (row e / W, slot e % W) <-> natural pixel of that row
+    auto nat = [&](int e) -> int {
+        const int r = e / W;
+        return r * W + rev[e - r * W];
+    };
+    auto ain = [&](int px) -> double { return a.ain ? (double)a.ain[pix0 + px] : 1.0; };
+    constexpr bool GATHER = OP == RO_FWD || OP == RO_INV || OP == RO_WARM || OP == RO_GD_INIT;
+    for (int e = threadIdx.x; e < ne; e += kThreads) {
+        double2 v;
+        if constexpr (GATHER) {
+            const int px = nat(e);
+            if constexpr (OP == RO_WARM) {
+                // numpy: exp(1j * float32 phase) is complex64, then times the float64 a_in
+                double s, c;
+                sincos((double)a.phase_in[off + px], &s, &c);
+                const double am = ain(px);
+                v = make_double2((double)(float)c * am, (double)(float)s * am);
+            } else if constexpr (OP == RO_GD_INIT) {
+                const float2 f = a.field0[off + px];
+                const double2 x = make_double2((double)f.x, (double)f.y);
+                a.x[off + px] = x;
+                v = u_of(x, ain(px));
+            } else {
+                v = a.in[off + px];
+            }
+        } else {
+            v = a.in[off + e];
+        }
+        lds[e] = v;
+    }
+    __syncthreads();
+    const Lines g{rows, W, 1};
+    if constexpr (GATHER) {
+        fft_dit<OP == RO_INV, false>(lds, g, a.pl);
+    } else {
+        fft_dif<true, false>(lds, g, a.pl);  // inverse: A (GS), the gradient (GD), A0 (setup)
+        // projection on the digit-reversed order, between the inverse and the forward transform
+        const bool phase_only = OP == RO_GS && (a.last || (a.checked && a.stop[b] == a.iter));
+        const double l = OP == RO_GD ? (double)a.lr[a.iter] : 0.0;
+        for (int e = threadIdx.x; e < ne; e += kThreads) {
+            const int px = nat(e);
+            const double2 z = lds[e];
+            if constexpr (OP == RO_COLD) {
+                lds[e] = unit_of(round_c64(z), ain(px));  // A0 = ifft2(sqrt T) is complex64 (:27)
+            } else if constexpr (OP == RO_GS) {
+                if (phase_only)
+                    a.phase_out[off + px] = (float)atan2(z.y, z.x);  // hologram = np.angle(A) (:48)
+                else
+                    lds[e] = unit_of(z, ain(px));
+            } else if constexpr (OP == RO_GD_FOURIER) {
+                // angle of the complex64 ifft2 is float32, exp of it complex64 (:153-156)
+                const double2 c = round_c64(z);
+                const float ang = atan2f((float)c.y, (float)c.x);
+                double s, co;
+                sincos((double)ang, &s, &co);
+                const double am = ain(px);
+                const double2 x = make_double2((double)(float)co * am, (double)(float)s * am);
+                a.x[off + px] = x;
+                lds[e] = u_of(x, am);
+            } else if constexpr (OP == RO_GD) {
+                // dEdF = ifft2(G) a_in (unscaled transform * 1/S), dEdX_complex, x -= lr dEdX
+                const double am = ain(px);
+                const double s = am * a.inv_s;
+                const double gx = z.x * s, gy = z.y * s;
+                double2 x = a.x[off + px];
+                const double ax2 = x.x * x.x + x.y * x.y;
+                const double ax = sqrt(ax2);
+                const double re = x.x * gx + x.y * gy;
+                x.x -= l * ((gx - x.x * (re / ax2)) / ax);
+                x.y -= l * ((gy - x.y * (re / ax2)) / ax);
+                a.x[off + px] = x;
+                lds[e] = u_of(x, am);
+            }
+        }
+        // (uniform per workgroup) the run's last GD update needs no next forward transform
+        if (phase_only || (OP == RO_GD && a.last)) return;
+        __syncthreads();
+        fft_dit<false, false>(lds, g, a.pl);
+    }
+    for (int e = threadIdx.x; e < ne; e += kThreads) a.out[off + e] = lds[e];
+}
+
+template <int OP>
+__global__ void __launch_bounds__(kThreads, MR_WPE) mr_col_kernel(ColArgs a) {
+    extern __shared__ double2 lds[];
+    const int b = blockIdx.x / a.nwg;
+    const int tile = blockIdx.x - b * a.nwg;
+    const int cw = 1 << a.cw_log2;
+    const int c0 = tile * cw;
+    const int ne = a.H * cw;
+    const long long hoff = (long long)b * a.holo;
+    const int* __restrict__ rev = a.pl.rev;
+    if constexpr (OP == CO_GS || OP == CO_GD_STATS || OP == CO_GD_GRAD) {
+        if (a.checked && a.iter > a.stop[b]) return;  // stopped earlier: frozen
+    }
+    // element e of the tile: LDS row h = e >> cw_log2, column c0 + (e & (cw - 1));
+    // global index at image row `row`
+    auto at = [&](int e, int row, long long& i) -> bool {
+        const int x = c0 + (e & (cw - 1));
+        i = hoff + (long long)row * a.W + x;
+        return x < a.W;
+    };
+    constexpr bool GATHER = OP == CO_FWD || OP == CO_INV || OP == CO_AMP_INV;
+    for (int e = threadIdx.x; e < ne; e += kThreads) {
+        const int h = e >> a.cw_log2;
+        long long i;
+        double2 v = make_double2(0.0, 0.0);
+        if (at(e, GATHER ? rev[h] : h, i)) {
+            if constexpr (OP == CO_AMP_INV)
+                v = make_double2(amp_of(a.tgt, a.tt, i), 0.0);
+            else
+                v = a.in[i];
+        }
+        lds[e] = v;
+    }
+    __syncthreads();
+    const Lines g{cw, 1, cw};
+    if constexpr (GATHER) {
+        fft_dit<OP != CO_FWD, true>(lds, g, a.pl);
+    } else {
+        fft_dif<false, true>(lds, g, a.pl);  // C (GS), F (GD)
+        double mx = 0.0, s2 = 0.0, st = 0.0, s = 0.0;
+        if constexpr (OP == CO_GD_GRAD) s = a.norm[b] / a.stats[((long long)b * a.max_loops + a.iter) * 4];
+        for (int e = threadIdx.x; e < ne; e += kThreads) {
+            long long i;
+            if (!at(e, rev[e >> a.cw_log2], i)) continue;  // frequency row of this position
+            const double2 z = lds[e];
+            const double en = z.x * z.x + z.y * z.y;
+            const double t = t_of(a.tgt, a.tt, i);
+            if constexpr (OP == CO_GS || OP == CO_GD_STATS) {
+                mx = fmax(mx, en);
+                s2 += en * en;
+                st += en * t;
+                if (a.write_e) a.e_out[i] = (float)en;
+            }
+            if constexpr (OP == CO_GS) {
+                lds[e] = unit_of(z, amp_of(a.tgt, a.tt, i));  // D = a_T C/|C| (:33)
+            } else if constexpr (OP == CO_GD_GRAD) {
+                // numpy's mask dtype: float32 for a float32 target, float64 for uint8 (:80)
+                const double mask = a.tt == TGT_U8 ? 1.0 + (double)a.wa * t / 255.0
+                                                   : (double)(1.0f + __fdiv_rn(__fmul_rn(a.wa, (float)t), 255.0f));
+                const double w = mask * (en * s - t);
+                lds[e] = make_double2(z.x * w, z.y * w);
+            }
+        }
+        if constexpr (OP == CO_GS || OP == CO_GD_STATS) {
+            block_reduce_stats<kThreads>(mx, s2, st);
+            if (threadIdx.x == 0) {
+                double* dst = a.partials + (((long long)b * a.max_loops + a.iter) * a.nwg + tile) * 4;
+                dst[0] = mx;
+                dst[1] = s2;
+                dst[2] = st;
+                dst[3] = 0.0;
+            }
+        }
+        if constexpr (OP == CO_GD_STATS) return;
+        __syncthreads();
+        fft_dit<true, true>(lds, g, a.pl);
+    }
+    for (int e = threadIdx.x; e < ne; e += kThreads) {
+        long long i;
+        if (at(e, e >> a.cw_log2, i)) a.out[i] = lds[e];
+    }
+}
+
+// dynamic LDS above 64 KiB must be allowed per kernel (once per process and kernel)
+template <class F>
+bool raise_lds(F fn) {
+    return hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLine * 16) ==
+           hipSuccess;
+}
+
+template <int OP>
+int row_one(const RowArgs& a, int grid, size_t lds, hipStream_t st) {
+    static const bool ok = raise_lds(mr_row_kernel<OP>);
+    if (!ok) return -1;
+    hipLaunchKernelGGL(mr_row_kernel<OP>, dim3(grid), dim3(kThreads), lds, st, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+template <int OP>
+int col_one(const ColArgs& a, int grid, size_t lds, hipStream_t st) {
+    static const bool ok = raise_lds(mr_col_kernel<OP>);
+    if (!ok) return -1;
+    hipLaunchKernelGGL(mr_col_kernel<OP>, dim3(grid), dim3(kThreads), lds, st, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace
+
+int mr_row_launch(int op, const RowArgs& a, int grid, size_t lds, hipStream_t st) {
+    switch (op) {
+        case RO_FWD: return row_one<RO_FWD>(a, grid, lds, st);
+        case RO_INV: return row_one<RO_INV>(a, grid, lds, st);
+        case RO_COLD: return row_one<RO_COLD>(a, grid, lds, st);
+        case RO_WARM: return row_one<RO_WARM>(a, grid, lds, st);
+        case RO_GS: return row_one<RO_GS>(a, grid, lds, st);
+        case RO_GD_FOURIER: return row_one<RO_GD_FOURIER>(a, grid, lds, st);
+        case RO_GD_INIT: return row_one<RO_GD_INIT>(a, grid, lds, st);
+        case RO_GD: return row_one<RO_GD>(a, grid, lds, st);
+        default: return -1;
+    }
+}
+int mr_col_launch(int op, const ColArgs& a, int grid, size_t lds, hipStream_t st) {
+    switch (op) {
+        case CO_FWD: return col_one<CO_FWD>(a, grid, lds, st);
+        case CO_INV: return col_one<CO_INV>(a, grid, lds, st);
+        case CO_AMP_INV: return col_one<CO_AMP_INV>(a, grid, lds, st);
+        case CO_GS: return col_one<CO_GS>(a, grid, lds, st);
+        case CO_GD_STATS: return col_one<CO_GD_STATS>(a, grid, lds, st);
+        case CO_GD_GRAD: return col_one<CO_GD_GRAD>(a, grid, lds, st);
+        default: return -1;
+    }
+}
+int mr_set_roots(const double2* roots, hipStream_t st) {
+    if (hipMemcpyToSymbolAsync(HIP_SYMBOL(kRoots), roots, sizeof(kRoots), 0, hipMemcpyHostToDevice, st) != hipSuccess)
+        return -1;
+    return hipStreamSynchronize(st) == hipSuccess ? 0 : -1;
+}
+
+}  // namespace mr
+}  // namespace slm

@@ -808,6 +808,26 @@ int recover_grid_fault(slm_plan* p, bool* faulted) {
     return 0;
 }
 
+// GenericView::mark of timed runs: each marked launch between an event pair on
+// the plan stream (the DFT-GEMM / mixed-radix engine launches directly)
+int generic_mark(void* ctx, int cls, int begin) {
+    slm_plan* p = static_cast<slm_plan*>(ctx);
+    if (begin) {
+        if (p->ev_used == p->ev_pool.size()) {
+            hipEvent_t a, b;
+            HIP_TRY(hipEventCreate(&a));
+            HIP_TRY(hipEventCreate(&b));
+            p->ev_pool.emplace_back(a, b);
+            p->ev_class.push_back(cls);
+        }
+        p->ev_class[p->ev_used] = cls;
+        HIP_TRY(hipEventRecord(p->ev_pool[p->ev_used].first, p->stream));
+    } else {
+        HIP_TRY(hipEventRecord(p->ev_pool[p->ev_used++].second, p->stream));
+    }
+    return 0;
+}
+
 GenericView gview(slm_plan* p) {
     GenericView v;
     v.algo = p->algo;
@@ -832,6 +852,10 @@ GenericView gview(slm_plan* p) {
     v.stop = p->stop;
     v.norm = p->norm;
     v.sum_t2 = p->sum_t2;
+    if (p->timing) {  // slm_plan_run_timed: one event pair per iteration launch
+        v.mark = &generic_mark;
+        v.mark_ctx = p;
+    }
     return v;
 }
 
@@ -1018,7 +1042,7 @@ int plan_create_on(int device, int algo, int batch, int height, int width, int t
         p->prec = PREC_F64;
         p->lid = LAYOUT_DEFAULT;
         p->cw = 0;
-        p->nwg = max_nwg = generic_nwg(p->holo);
+        p->nwg = max_nwg = generic_nwg(height, width, p->holo);
         p->rpw = min_rpw = 1;
     } else {
         const int want = p->prec;
@@ -1247,7 +1271,7 @@ int slm_plan_run(slm_plan* p, int loops, double tol, int checked, float wa) {
         const char* e = std::getenv("SLM_GRAPH");
         return !e || std::atoi(e) != 0;
     }();
-    if (!p || !use_graph || p->gen) {  // rocBLAS calls: not captured
+    if (!p || !use_graph || generic_uses_blas(p->gen)) {  // rocBLAS calls: not captured
         RC(enqueue_run(p, loops, tol, checked, wa));
         if (p && p->gfault && gd_fused_fn(p, checked)) p->fused_pending = true;
         return 0;
@@ -1397,10 +1421,20 @@ int slm_plan_set_target_stats(slm_plan* p, const double* norm, const double* sum
 
 long long slm_plan_kernel_bytes(slm_plan* p, int cls) {
     if (!p) return -1;
-    if (p->gen) return 0;  // the DFT-GEMM engine has no column / row kernel classes
     const long long px = (long long)p->B * p->holo;
     const long long tb = p->tt == SLM_TGT_U8 ? 1 : 4;
     const long long ab = p->has_ain ? 4 : 0;
+    if (p->gen) {
+        if (generic_uses_blas(p->gen)) return 0;  // DFT-GEMM: no column / row kernel classes
+        // mixed radix, complex128 state: column pass in 16 + T + out 16 (GD statistics: in + T);
+        // row pass in 16 + out 16 (+ a_in) (+ GD field read and write 32)
+        switch (cls) {
+            case SLM_KERNEL_COL_MAIN: return px * (32 + tb);
+            case SLM_KERNEL_ROW_MAIN: return px * (32 + ab + (p->algo == SLM_ALGO_GD ? 32 : 0));
+            case SLM_KERNEL_GD_STATS: return px * (16 + tb);
+            default: return 0;
+        }
+    }
     const bool lin = p->algo == SLM_ALGO_GD && p->gd_mode == GD_LIN;  // + Y2 out (column) / in (row)
     switch (cls) {
         case SLM_KERNEL_COL_MAIN: return px * (8 + tb + 8 + (lin ? 8 : 0));  // X (GD: F) in, T in, Y out
@@ -1428,7 +1462,7 @@ int slm_plan_engine(slm_plan* p, int* col_engine, int* row_engine) {
     if (!p || !col_engine || !row_engine) return fail(SLM_ERR_ARG, "null argument");
     // mirrors kernels.hpp: kShuffle<K, P> && (CW == 2 | RPW == 2) && one line per thread
     if (p->gen) {
-        *col_engine = *row_engine = 2;  // DFT-GEMM (generic.hpp)
+        *col_engine = *row_engine = generic_uses_blas(p->gen) ? 2 : 3;  // DFT-GEMM / mixed radix (generic.hpp)
         return 0;
     }
     auto shuf = [&](int key) {
@@ -1603,6 +1637,41 @@ int slm_fft2(const float* in, float* out, int batch, int height, int width, int 
         if (e != hipSuccess) rc = fail(SLM_ERR_HIP, "fft2 failed: %s", hipGetErrorString(e));
     }
     free_plan(p);
+    return rc;
+}
+
+int slm_fft2_c128(const double* in, double* out, int batch, int height, int width, int inverse) {
+    if (!in || !out) return fail(SLM_ERR_ARG, "null argument");
+    if (batch < 1 || height < 1 || width < 1) return fail(SLM_ERR_ARG, "shape %d x %d x %d", batch, height, width);
+    RC(ensure_device());
+    HIP_TRY(hipSetDevice(g_device));
+    // the float64 engine of the any-size plans (mixed radix where the sides
+    // factor, else DFT-GEMM), whatever the shape: a scratch GS view of its own
+    slm_plan q;
+    q.algo = SLM_ALGO_GS;
+    q.B = batch;
+    q.H = height;
+    q.W = width;
+    q.holo = (long long)height * width;
+    q.max_loops = 1;
+    q.nwg = generic_nwg(height, width, q.holo);
+    q.device = g_device;
+    HIP_TRY(hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking));
+    const size_t bytes = (size_t)batch * q.holo * sizeof(double2);
+    double2* buf = nullptr;
+    GenericEngine* g = nullptr;
+    int rc = 0;
+    if (hipMalloc(&buf, bytes) != hipSuccess) rc = fail(SLM_ERR_HIP, "fft2_c128: allocation of %zu bytes", bytes);
+    if (!rc) rc = generic_create(gview(&q), &g);
+    if (!rc && hipMemcpyAsync(buf, in, bytes, hipMemcpyHostToDevice, q.stream) != hipSuccess)
+        rc = fail(SLM_ERR_HIP, "fft2_c128: upload failed");
+    if (!rc) rc = generic_fft2_z(g, gview(&q), buf, buf, inverse);
+    if (!rc) rc = copy_sync(out, buf, bytes, hipMemcpyDeviceToHost, q.stream);
+    (void)hipStreamSynchronize(q.stream);
+    generic_destroy(g);
+    if (buf) (void)hipFree(buf);
+    (void)hipStreamDestroy(q.stream);
+    q.stream = nullptr;
     return rc;
 }
 

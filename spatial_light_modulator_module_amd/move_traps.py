@@ -5,7 +5,8 @@ DESIGN.md section 7).
 * ``update_hologram(black_image, coords, which)`` — src/move_traps.py:64-68:
   the phase of ``ifft2`` of a blank image with one 255-valued pixel, float64,
   computed on the GPU by slm_trap_frames (closed form of the single-pixel
-  inverse DFT, exact integer phase index; no transform needed).
+  inverse DFT, exact integer phase index; no transform needed); an image that
+  already holds traps takes the float64 device transform (slm_fft2_c128).
 * ``hologram_frame(hologram, mask, mask_flag, ct2pi)`` — the quantisation of
   display_hologram, src/move_traps.py:135-139, as the uint8 frame handed to the
   SLM window.
@@ -32,9 +33,8 @@ def update_hologram(black_image: np.ndarray, coords, which) -> np.ndarray:
     float64; the pixel under the trap is left at 0 afterwards, as the reference
     leaves it. A blank image (the reference's loop, src/move_traps.py:16) takes
     the closed form (slm_trap_frames, exact phase index). Any other image runs
-    the device's inverse 2-D transform in complex64 (slm_fft2): the phase is then
-    as accurate as the field's float32 rounding allows (~1e-7 of the field's
-    largest value; tests/test_frames.py)."""
+    the device's float64 inverse 2-D transform (slm_fft2_c128), as the
+    reference's float64 ifft2 does (tests/test_frames.py)."""
     black_image = np.asarray(black_image)
     if black_image.ndim != 2:
         raise ValueError("black_image must be a 2-D image")
@@ -44,9 +44,11 @@ def update_hologram(black_image: np.ndarray, coords, which) -> np.ndarray:
         black_image[y][x] = 0
         return phase[0]
     black_image[y][x] = 255
-    field = _lib.fft2(black_image.astype(np.complex64), inverse=True)  # unscaled: the 1/(h w) leaves angles alone
+    # float64 on the device, as the reference's ifft2 of the float64 image (unscaled:
+    # the 1/(h w) leaves angles alone)
+    field = _lib.fft2_c128(black_image.astype(np.complex128), inverse=True)
     black_image[y][x] = 0
-    return np.angle(field).astype(np.float64)
+    return np.angle(field)
 
 
 def hologram_frame(hologram: np.ndarray, mask, mask_flag: bool, ct2pi) -> np.ndarray:

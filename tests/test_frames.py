@@ -89,8 +89,9 @@ def test_trap_phase_matches_reference(gpu, shape):
 @pytest.mark.parametrize("shape", [(256, 256), (768, 1024), (90, 150)])
 def test_update_hologram_non_blank(gpu, shape):
     """An image already holding traps (src/move_traps.py:64-68 with a non-blank
-    black_image): angle(ifft2) through the device transform (complex64) vs the
-    float64 reference restatement, where the field is not near zero."""
+    black_image): angle(ifft2) through the device's float64 transform
+    (slm_fft2_c128) vs the float64 reference restatement at EVERY pixel --
+    the SLM shows the phase wherever the field is dim too."""
     from spatial_light_modulator_module_amd import move_traps as mt
 
     rng = np.random.default_rng(11)
@@ -102,12 +103,15 @@ def test_update_hologram_non_blank(gpu, shape):
     lit = img.astype(np.float64)
     lit[y, x] = 255
     field = np.fft.ifft2(lit)
-    keep = np.abs(field) > 1e-2 * np.abs(field).max()
+    # a float64 transform's angle error is ~1e-16 max|field| / |field|: every pixel
+    # whose field is not itself at rounding level (none of these images has one)
+    keep = np.abs(field) > 1e-9 * np.abs(field).max()
     got = mt.update_hologram(img, [[y, x]], 0)
     assert got.dtype == np.float64 and got.shape == shape
     err = wrapped(got, ref)[keep].max()
-    print(f"[parity] non-blank update_hologram {shape}: max wrapped phase error {err:.2e} on {keep.mean():.3f} of pixels")
-    assert err < 1e-3
+    print(f"[parity] non-blank update_hologram {shape}: max wrapped phase error {err:.2e} on {keep.mean():.6f} "
+          f"of pixels (smallest |field| / max {np.abs(field).min() / np.abs(field).max():.2e})")
+    assert keep.mean() > 0.999 and err < 1e-6
     np.testing.assert_array_equal(img, want_img)  # the trap pixel is back at 0, the rest untouched
 
 
