@@ -72,9 +72,9 @@ def launch_ranks(n: int) -> int:
     return max(abs(rc) for rc in rcs)
 
 
-def targets(first: int, count: int, n: int) -> np.ndarray:
-    """T_b = default_rng(1234 + b).uniform(0, 255, (n, n)) float32."""
-    return np.stack([np.random.default_rng(1234 + b).uniform(0, 255, (n, n)).astype(np.float32)
+def targets(first: int, count: int, n: int, w: int | None = None) -> np.ndarray:
+    """T_b = default_rng(1234 + b).uniform(0, 255, (n, w or n)) float32."""
+    return np.stack([np.random.default_rng(1234 + b).uniform(0, 255, (n, w or n)).astype(np.float32)
                      for b in range(first, first + count)])
 
 
@@ -160,6 +160,7 @@ def rank_diagnostics(plan, counts, rank, local_elapsed, steps, rows):
     kern = {k: round(v["avg_us"], 3) for k, v in rows.items()}
     run_us = sum(v["total_us"] for v in rows.values())
     return {"rank": rank, "device": dev, "pci_bus_id": bus, "holograms": int(counts[rank]),
+            "gather_stream": "comm stream behind a staging copy (overlaps the next run)",
             "step_ms": round(local_elapsed / steps * 1e3, 4), "kernel_avg_us": kern,
             "iteration_kernels_ms_per_run": round(run_us / 1e3, 4),
             "gather_ms": round(gather_ms, 4), "gather_bytes_to_root": gather_bytes,
@@ -254,12 +255,13 @@ def _round(v):
     return round(v, 4) if isinstance(v, float) else v
 
 
-def secondary(n, batch, iters, algo=_lib.ALGO_GS, precision=None, reps=3):
+def secondary(n, batch, iters, algo=_lib.ALGO_GS, precision=None, reps=3, width=None):
     """Extra single-GPU measurements: one-run wall time and the per-kernel
     roofline of another configuration (4096^2 HBM stress, batched 1024^2, GD,
-    float64 butterflies)."""
-    t = targets(0, batch, n)
-    with _lib.Plan(algo, batch, n, n, _lib.TGT_F32, False, iters) as plan:
+    float64 butterflies, an n x width SLM panel on the any-size engine)."""
+    w = width or n
+    t = targets(0, batch, n, w)
+    with _lib.Plan(algo, batch, n, w, _lib.TGT_F32, False, iters) as plan:
         plan.set_target(t)
         if precision is not None:
             plan.set_precision(precision)
@@ -279,17 +281,18 @@ def secondary(n, batch, iters, algo=_lib.ALGO_GS, precision=None, reps=3):
         wall = (time.perf_counter() - t0) / reps
         dom, rows, _, _ = kernel_roofline(plan, iters, wa)
         info = plan.info()
+        plan_engine = plan.engine()
     iter_s = wall / iters
     # bytes the launches of one iteration physically move (slm_plan_kernel_bytes)
     phys_iter = sum(r["physical_bytes_per_launch"] for r in rows.values())
     name = "gd" if algo == _lib.ALGO_GD else "gs"
-    traffic = pmc_traffic(f"{name}_{n}x{n}_b{batch}_it{iters}_{info['precision']}")  # rocprofv3 PMC, profiles/
+    traffic = pmc_traffic(f"{name}_{n}x{w}_b{batch}_it{iters}_{info['precision']}")  # rocprofv3 PMC, profiles/
     for k, row in rows.items():
         row["traffic_bytes_per_launch"] = None if traffic is None else traffic.get(k)
     per_px = 76 if algo == _lib.ALGO_GD else 68
-    return {"algo": name, "shape": [batch, n, n], "iters": iters,
+    return {"algo": name, "shape": [batch, n, w], "iters": iters, "engine": list(plan_engine),
             "holograms_per_s": batch / wall, "iter_ms": iter_s * 1e3, "iter_ms_per_hologram": iter_s * 1e3 / batch,
-            "iter_frac_of_hbm_peak_model": round(per_px * batch * n * n / iter_s / 1e9 / HBM_PEAK_GBS, 4),
+            "iter_frac_of_hbm_peak_model": round(per_px * batch * n * w / iter_s / 1e9 / HBM_PEAK_GBS, 4),
             "iter_frac_of_hbm_peak_physical": round(phys_iter / iter_s / 1e9 / HBM_PEAK_GBS, 4),
             "kernels": {k: {kk: _round(vv) for kk, vv in v.items()} for k, v in rows.items()}, "dominant": dom,
             "dominant_frac_of_hbm_peak_model": round(rows[dom]["achieved_gbs"] / HBM_PEAK_GBS, 4),
@@ -456,6 +459,8 @@ def main():
         extra = {"pcie_inclusive": pcie_inclusive(plan, targets(0, bper, n), iters)}
         try:  # every line at its BASELINE.json config's own iteration count
             extra["gs_256_it50"] = secondary(256, 1, 50, reps=20)  # configs[0]'s workload on the GPU
+            # a 1080 x 1920 SLM panel (no float32 radix plan): the float64 mixed-radix engine
+            extra["gs_1080x1920"] = secondary(1080, 1, 200, width=1920, reps=2)
             extra["gs_4096"] = secondary(4096, 1, 200)  # north-star shape, one hologram
             extra["gs_4096_batch8"] = secondary(4096, 8, 200)  # configs[4] per GPU at 8 GPUs
             extra["gs_1024_batch64"] = secondary(1024, 64, 200)  # configs[3] per GPU at 8 GPUs

@@ -343,6 +343,18 @@ struct slm_plan {
     long long gather_stats_elems = 0;
     int* gather_stop = nullptr;
     long long gather_stop_elems = 0;
+    // gathers run on their own stream behind a staging copy, so a rank's next
+    // run (plan stream) overlaps the RCCL transfer of the previous step's slab:
+    // two staging buffers, used alternately; the copy into one waits for the
+    // send that last read it (gather_done)
+    hipStream_t comm_stream = nullptr;
+    hipEvent_t gather_ready = nullptr;
+    hipEvent_t gather_done[2] = {nullptr, nullptr};
+    bool gather_done_set[2] = {false, false};
+    int gather_last = -1;            // slot of the last gather (its done event orders marks / timing)
+    void* stage[2] = {nullptr, nullptr};
+    size_t stage_cap[2] = {0, 0};
+    int stage_next = 0;
     bool target_set = false, phase_set = false, field_set = false, lr_set = false;
     // timing state (slm_plan_run_timed)
     bool timing = false;
@@ -885,6 +897,7 @@ void free_plan(slm_plan* p) {
     // work still queued on the plan stream (an unsynchronised run, a
     // stream-ordered device gather or RCCL send) finishes before its buffers go
     if (p->stream) (void)hipStreamSynchronize(p->stream);
+    if (p->comm_stream) (void)hipStreamSynchronize(p->comm_stream);  // gathers still reading / writing
     for (void* ptr : {(void*)p->xa, (void*)p->xb, (void*)p->y, (void*)p->field, p->tgt, (void*)p->ain,
                       (void*)p->phase_in, (void*)p->phase_out, (void*)p->e_out, (void*)p->partials,
                       (void*)p->stats, (void*)p->stop, (void*)p->norm, (void*)p->normf, (void*)p->sum_t2,
@@ -896,6 +909,12 @@ void free_plan(slm_plan* p) {
         (void)hipEventDestroy(e.first);
         (void)hipEventDestroy(e.second);
     }
+    for (int k = 0; k < 2; ++k) {
+        if (p->stage[k]) (void)hipFree(p->stage[k]);
+        if (p->gather_done[k]) (void)hipEventDestroy(p->gather_done[k]);
+    }
+    if (p->gather_ready) (void)hipEventDestroy(p->gather_ready);
+    if (p->comm_stream) (void)hipStreamDestroy(p->comm_stream);
     if (p->gexec) (void)hipGraphExecDestroy(p->gexec);
     generic_destroy(p->gen);
     for (hipEvent_t e : p->marks)
@@ -1351,6 +1370,7 @@ int slm_plan_sync(slm_plan* p) {
     if (!p) return fail(SLM_ERR_ARG, "null plan");
     HIP_TRY(hipSetDevice(p->device));
     HIP_TRY(hipStreamSynchronize(p->stream));
+    if (p->comm_stream) HIP_TRY(hipStreamSynchronize(p->comm_stream));  // queued gathers
     bool faulted = false;
     RC(recover_grid_fault(p, &faulted));
     if (faulted) {  // the last run again, on the two-launch column side (cannot fault)
@@ -1366,6 +1386,8 @@ int slm_plan_mark(slm_plan* p, int which) {
     if (!p || which < 0 || which > 1) return fail(SLM_ERR_ARG, "bad mark arguments");
     HIP_TRY(hipSetDevice(p->device));
     if (!p->marks[which]) HIP_TRY(hipEventCreate(&p->marks[which]));
+    // the stopwatch covers the gathers queued on the comm stream too
+    if (p->gather_last >= 0) HIP_TRY(hipStreamWaitEvent(p->stream, p->gather_done[p->gather_last], 0));
     HIP_TRY(hipEventRecord(p->marks[which], p->stream));
     return 0;
 }
@@ -1776,8 +1798,11 @@ namespace {
 // Gather one per-hologram slab of every rank to `root` (rank order): `src`
 // holds this rank's counts[me] x per_item elements of `elem` bytes (RCCL type
 // `dt`); on root the concatenation lands in *dev_buf (grown as needed) and,
-// if host_out, on the host. Grouped ncclSend / ncclRecv on the plan stream
-// (one xGMI hop per peer), synchronised before returning.
+// if host_out, on the host. The slab is first copied into a staging buffer on
+// the plan stream (so the next run, queued behind that copy, may overwrite
+// `src`), then the comm stream -- behind an event -- moves it: grouped
+// ncclSend / ncclRecv (one xGMI hop per peer), the root's own slab a device
+// copy. Stream-ordered, no host synchronisation unless host_out.
 int gather_slab(slm_plan* p, const void* src, long long per_item, size_t elem, ncclDataType_t dt, const int* counts,
                 int root, void** dev_buf, long long* dev_cap, void* host_out) {
     if (!p || !counts) return fail(SLM_ERR_ARG, "null argument");
@@ -1793,9 +1818,32 @@ int gather_slab(slm_plan* p, const void* src, long long per_item, size_t elem, n
     if (p->fused_pending) RC(slm_plan_sync(p));
     std::vector<long long> off(n + 1);
     RC(slm_gather_layout(n, counts, per_item, off.data()));
+    if (!p->comm_stream) {
+        HIP_TRY(hipStreamCreateWithFlags(&p->comm_stream, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&p->gather_ready, hipEventDisableTiming));
+        for (int k = 0; k < 2; ++k) HIP_TRY(hipEventCreateWithFlags(&p->gather_done[k], hipEventDisableTiming));
+    }
+    const size_t mine = (size_t)(off[me + 1] - off[me]) * elem;
+    const int k = p->stage_next;
+    p->stage_next ^= 1;
+    if (p->stage_cap[k] < mine) {
+        HIP_TRY(hipStreamSynchronize(p->comm_stream));  // nothing may still read the old buffer
+        if (p->stage[k]) HIP_TRY(hipFree(p->stage[k]));
+        p->stage[k] = nullptr;
+        p->stage_cap[k] = 0;
+        HIP_TRY(hipMalloc(&p->stage[k], mine));
+        p->stage_cap[k] = mine;
+    }
+    // plan stream: wait for the send that last read this staging buffer, copy the slab
+    if (p->gather_done_set[k]) HIP_TRY(hipStreamWaitEvent(p->stream, p->gather_done[k], 0));
+    if (mine) HIP_TRY(hipMemcpyAsync(p->stage[k], src, mine, hipMemcpyDeviceToDevice, p->stream));
+    HIP_TRY(hipEventRecord(p->gather_ready, p->stream));
+    hipStream_t cs = p->comm_stream;
+    HIP_TRY(hipStreamWaitEvent(cs, p->gather_ready, 0));
     if (me == root) {
         const long long elems = off[n];
         if (*dev_cap < elems) {
+            HIP_TRY(hipStreamSynchronize(cs));  // earlier gathers into the old buffer
             if (*dev_buf) HIP_TRY(hipFree(*dev_buf));
             *dev_buf = nullptr;
             *dev_cap = 0;
@@ -1808,21 +1856,27 @@ int gather_slab(slm_plan* p, const void* src, long long per_item, size_t elem, n
             const size_t cnt = (size_t)(off[r + 1] - off[r]);
             if (!cnt) continue;
             if (r == me) {
-                HIP_TRY(hipMemcpyAsync(dst + off[r] * elem, src, cnt * elem, hipMemcpyDeviceToDevice, p->stream));
+                HIP_TRY(hipMemcpyAsync(dst + off[r] * elem, p->stage[k], cnt * elem, hipMemcpyDeviceToDevice, cs));
             } else {
-                NCCL_TRY(ncclRecv(dst + off[r] * elem, cnt, dt, r, g_comm, p->stream));
+                NCCL_TRY(ncclRecv(dst + off[r] * elem, cnt, dt, r, g_comm, cs));
             }
         }
         if (n > 1) NCCL_TRY(ncclGroupEnd());
-        // a device-side gather stays stream-ordered (the next run on this
-        // stream, a read or slm_plan_sync wait for it); a host copy waits here
+        HIP_TRY(hipEventRecord(p->gather_done[k], cs));
+        p->gather_done_set[k] = true;
+        p->gather_last = k;
+        // a device-side gather stays stream-ordered (slm_plan_sync, a read or the
+        // stopwatch wait for it); a host copy waits here
         if (host_out && elems) {
-            HIP_TRY(hipStreamSynchronize(p->stream));
-            RC(copy_sync(host_out, dst, (size_t)elems * elem, hipMemcpyDeviceToHost, p->stream));
+            HIP_TRY(hipStreamSynchronize(cs));
+            RC(copy_sync(host_out, dst, (size_t)elems * elem, hipMemcpyDeviceToHost, cs));
         }
     } else {
         if (!g_comm) return fail(SLM_ERR_COMM, "no communicator");
-        if (p->B) NCCL_TRY(ncclSend(src, (size_t)p->B * per_item, dt, root, g_comm, p->stream));
+        if (p->B) NCCL_TRY(ncclSend(p->stage[k], (size_t)p->B * per_item, dt, root, g_comm, cs));
+        HIP_TRY(hipEventRecord(p->gather_done[k], cs));
+        p->gather_done_set[k] = true;
+        p->gather_last = k;
     }
     return 0;
 }
@@ -1848,6 +1902,9 @@ int slm_plan_time_gather(slm_plan* p, const int* counts, int root, int reps, dou
     float t = 0.f;
     if (hipEventRecord(e0, p->stream) != hipSuccess) rc = fail(SLM_ERR_HIP, "event record failed");
     for (int i = 0; i < reps && !rc; ++i) rc = slm_plan_gather_phase(p, counts, root, nullptr);
+    // the transfers run on the comm stream: the stop event follows the last one
+    if (!rc && p->gather_last >= 0 && hipStreamWaitEvent(p->stream, p->gather_done[p->gather_last], 0) != hipSuccess)
+        rc = fail(SLM_ERR_HIP, "gather timing wait failed");
     if (!rc && (hipEventRecord(e1, p->stream) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
                 hipEventElapsedTime(&t, e0, e1) != hipSuccess))
         rc = fail(SLM_ERR_HIP, "gather timing events failed");

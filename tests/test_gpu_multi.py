@@ -172,3 +172,40 @@ def test_multi_gpu_diagnostics(gpu):
         assert p.device == 0
     bus = lib.pci_bus_id(0)
     assert len(bus) >= 7 and ":" in bus
+
+
+@pytest.mark.gpu
+def test_gather_overlaps_next_run_stream_ordered(gpu):
+    """The phase gather stages the slab on the plan stream and moves it on the
+    plan's comm stream (two staging buffers, used alternately), so the next
+    run is queued right behind the staging copy. Each gather must still carry
+    the phases of the run before it, bit for bit, whatever runs are queued
+    behind it and however the staging buffers alternate: run -> gather ->
+    run -> gather -> gather, with no host synchronisation in between until
+    the host copies (src/generate_hologram_sequence.py:19-31 is the loop)."""
+    lib = gpu
+    loops = 7
+    ta, tb = _targets(2, 256, False), _targets(2, 256, False)[::-1].copy()
+    with lib.Plan(lib.ALGO_GS, 2, 256, 256, lib.TGT_F32, False, loops) as p:
+        p.set_target(ta)
+        p.run(loops)
+        want_a = p.read(expected=False, stats=False, iters=False)[0]
+        p.set_target(tb)
+        p.run(loops)
+        want_b = p.read(expected=False, stats=False, iters=False)[0]
+        got = []
+        for t in (ta, tb, ta):
+            p.set_target(t)
+            p.run(loops)
+            p.gather_phase([2], 0)              # stage k, device only: no host sync
+            buf = np.empty((2, 256, 256), np.float32)
+            p.run(loops)                        # queued behind the staging copy, overlaps the transfer
+            p.gather_phase([2], 0, buf)         # stage k ^ 1, then the host copy
+            got.append(buf)
+        p.mark(0)
+        p.gather_phase([2], 0)
+        p.mark(1)
+        assert p.marked_ms() >= 0.0  # the stopwatch waits for the comm stream's gather
+    np.testing.assert_array_equal(got[0], want_a)
+    np.testing.assert_array_equal(got[1], want_b)
+    np.testing.assert_array_equal(got[2], want_a)
