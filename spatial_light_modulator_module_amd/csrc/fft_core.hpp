@@ -25,12 +25,6 @@
 
 #include "plans.hpp"
 
-#ifndef SLM_LDS_SWZ
-#define SLM_LDS_SWZ 1
-#endif
-#ifndef SLM_COL_LINE_MAJOR
-#define SLM_COL_LINE_MAJOR 1
-#endif
 
 namespace slm {
 
@@ -69,9 +63,9 @@ struct PlanOf {
     static constexpr int LINE = lds_line(N);
     // row stride of per-line LDS regions (LdsLine): == 16 (mod 32) complex, so
     // the two rows served by one 32-lane ds_read_b64 group hit disjoint halves
-    // of the banks. Lines are XOR-swizzled, not padded (SLM_LDS_SWZ), so the
+    // of the banks. Lines are XOR-swizzled, not padded (lds_slot), so the
     // region is N long.
-    static constexpr int LLEN = SLM_LDS_SWZ ? N : LINE;
+    static constexpr int LLEN = N;
     static constexpr int ROWSTRIDE = LLEN + ((16 - LLEN % 32) + 32) % 32;
 };
 
@@ -257,20 +251,14 @@ struct Dft<16, INV, C> {
 // wave passes after its reads of exchange k completed (lgkmcnt(0)). `cur` is
 // flipped in fully unrolled code from a constant start, so it folds into the
 // ds_read / ds_write offsets.
-// Element slot of a line in a per-line region. SLM_LDS_SWZ: XOR-swizzle the
-// low 4 index bits with bits 4..7 (a bijection inside each 16-element block):
-// the pass-1 writes (o = 16 t + r), the strided writes of later passes and the
+// Element slot of a line in a per-line region: XOR-swizzle the low 4 index
+// bits with bits 4..7 (a bijection inside each 16-element block): the pass-1
+// writes (o = 16 t + r), the strided writes of later passes and the
 // lane-contiguous reads (o = t + T m) all hit distinct banks in their
 // 16-lane write / 32-lane read groups (tools/lds_banks.py: 4096 rows 2.0 -> 0
-// extra cycles per read, 768 rows 2.0 -> 0.67 per write, nothing worse).
-// Otherwise one pad slot per 16 (lanes t and t + 16 of a read group collide).
-__device__ __forceinline__ int lds_slot(int o) {
-#if SLM_LDS_SWZ
-    return o ^ ((o >> 4) & 15);
-#else
-    return o + (o >> 4);
-#endif
-}
+// extra cycles per read, 768 rows 2.0 -> 0.67 per write, nothing worse than
+// one pad slot per 16, which it replaced).
+__device__ __forceinline__ int lds_slot(int o) { return o ^ ((o >> 4) & 15); }
 
 // WAVE: every line of the region is written and read by the threads of one
 // wave only (wave-line mappings, kernels.hpp), so an exchange needs no
@@ -346,52 +334,11 @@ struct TwCountOf<N, IntList<Rs...>> {
 //             kernel (float32 arithmetic: exact table values matter there);
 //  TW_DIRECT: read from the (L1/L2-resident) table where used, for 1024-thread
 //             workgroups whose 128-VGPR budget cannot hold a cache;
-//  TW_POWERS: float64 arithmetic: only w^1 of each butterfly is cached and the
-//             powers w^2..w^(R-1) are formed by multiplication (error ~1e-15,
-//             far below the complex64 storage rounding).
-//  TW_CHAIN:  as TW_POWERS, but w^r is formed incrementally as it is applied
-//             (w^r = w^(r-1) w), so only two twiddles are ever live.
-//  TW_LAST:   the last pass's twiddles cached in registers, earlier passes
-//             read from the (L1-resident, few-KB) table where used: fewer
-//             registers (4096 row kernel 194 -> 165 VGPRs, 3 waves per SIMD)
-//             but measured slower (4096^2 row pass 103 -> 117 us, 8 x 4096^2
-//             785 -> 968 us: the table loads sit in the dependency chain), and
-//             the compiler contracts the products differently (not bitwise
-//             TW_CACHED). Kept for A/B builds (-DSLM_F32_ROW_TW=4).
-//  TW_SPLIT:  radix-16 passes only: per butterfly group w^1..w^3 and w^4,
-//             w^8, w^12 cached (exact table values), w^(4a+b) = w^(4a) w^b
-//             formed where used (one complex product, one rounding): 6
-//             registers-pairs per group instead of 15 (4096 16.16.16 plans).
-enum TwMode : int { TW_CACHED = 0, TW_DIRECT = 1, TW_POWERS = 2, TW_CHAIN = 3, TW_LAST = 4, TW_SPLIT = 5 };
-
-template <int N, int Ns, int... Rs>
-struct TwPowCountImpl;
-template <int N, int Ns>
-struct TwPowCountImpl<N, Ns> {
-    static constexpr int value = 0;
-};
-template <int N, int Ns, int R, int... Rest>
-struct TwPowCountImpl<N, Ns, R, Rest...> {
-    static constexpr int value = (Ns > 1 ? PlanOf<N>::E / R : 0) + TwPowCountImpl<N, Ns * R, Rest...>::value;
-};
-template <int N, class L>
-struct TwPowCountOf;
-template <int N, int... Rs>
-struct TwPowCountOf<N, IntList<Rs...>> {
-    static constexpr int value = TwPowCountImpl<N, 1, Rs...>::value;
-};
-
-// w[r] = w^r for r = 1..R-1 from w[1], log-depth (w^(2k) = (w^k)^2, else
-// w^hi * w^(r-hi) with hi the highest power of two below r)
-template <int R, class C>
-__device__ __forceinline__ void twiddle_powers(C (&w)[R]) {
-    static_for<R - 2>([&](auto rc) {
-        constexpr int r = decltype(rc)::value + 2;
-        constexpr int hi = (r & (r - 1)) == 0 ? r / 2 : (1 << (31 - __builtin_clz(r)));
-        constexpr int lo = (r & (r - 1)) == 0 ? r / 2 : r - hi;
-        w[r] = cmul(w[hi], w[lo]);
-    });
-}
+//  (Forming w^2.. from w^1 in registers, caching the last pass only, and
+//  split radix-16 twiddles w^(4a) w^b were measured: faster variants moved
+//  the 4096^2 float32 warm-start parity past the bar, slower ones were slower;
+//  DESIGN.md sections 4-5.)
+enum TwMode : int { TW_CACHED = 0, TW_DIRECT = 1 };
 
 template <int N, class C, int MODE>
 struct Twiddles;
@@ -436,112 +383,6 @@ struct Twiddles<N, C, TW_DIRECT> {
         });
     }
 };
-template <int N, class C>
-struct Twiddles<N, C, TW_POWERS> {
-    static constexpr int COUNT = TwPowCountOf<N, RadicesOf<N>>::value > 0 ? TwPowCountOf<N, RadicesOf<N>>::value : 1;
-    C w1[COUNT];
-    __device__ __forceinline__ void launder() {}
-    template <int TwOff, int RegOff, int PowOff, int R, int Ns, bool INV>
-    __device__ __forceinline__ void apply(C* u, int k, int) const {
-        C w[R];
-        w[1] = w1[PowOff + k];
-        twiddle_powers<R>(w);
-        static_for<R - 1>([&](auto rc) {
-            constexpr int r = decltype(rc)::value + 1;
-            u[r] = INV ? cmulc(u[r], w[r]) : cmul(u[r], w[r]);
-        });
-    }
-};
-
-template <int N, class C>
-struct Twiddles<N, C, TW_CHAIN> {
-    static constexpr int COUNT = TwPowCountOf<N, RadicesOf<N>>::value > 0 ? TwPowCountOf<N, RadicesOf<N>>::value : 1;
-    C w1[COUNT];
-    __device__ __forceinline__ void launder() {}
-    template <int TwOff, int RegOff, int PowOff, int R, int Ns, bool INV>
-    __device__ __forceinline__ void apply(C* u, int k, int) const {
-        const C b = w1[PowOff + k];
-        C w = b;
-        static_for<R - 1>([&](auto rc) {
-            constexpr int r = decltype(rc)::value + 1;
-            u[r] = INV ? cmulc(u[r], w) : cmul(u[r], w);
-            if constexpr (r + 1 < R) w = cmul(w, b);
-        });
-    }
-};
-
-// TW_LAST: register slots of the last pass only
-template <int N, int Ns, int... Rs>
-struct TwLastCountImpl;
-template <int N, int Ns, int R>
-struct TwLastCountImpl<N, Ns, R> {
-    static constexpr int value = Ns > 1 ? (PlanOf<N>::E / R) * (R - 1) : 0;
-};
-template <int N, int Ns, int R, int R2, int... Rest>
-struct TwLastCountImpl<N, Ns, R, R2, Rest...> {
-    static constexpr int value = TwLastCountImpl<N, Ns * R, R2, Rest...>::value;
-};
-template <int N, class L>
-struct TwLastCountOf;
-template <int N, int... Rs>
-struct TwLastCountOf<N, IntList<Rs...>> {
-    static constexpr int value = TwLastCountImpl<N, 1, Rs...>::value;
-};
-
-template <int N, class C>
-struct Twiddles<N, C, TW_LAST> {
-    static constexpr int COUNT = TwLastCountOf<N, RadicesOf<N>>::value > 0 ? TwLastCountOf<N, RadicesOf<N>>::value : 1;
-    struct alignas(2 * sizeof(Scalar<C>)) Pod {
-        Scalar<C> x, y;
-    };
-    using GlobalPtr = const __attribute__((address_space(1))) Pod*;
-    C w[COUNT];
-    GlobalPtr table;
-    __device__ __forceinline__ void launder() {
-        unsigned long long q = (unsigned long long)table;
-        asm volatile("" : "+s"(q));
-        table = (GlobalPtr)q;
-    }
-    template <int TwOff, int RegOff, int PowOff, int R, int Ns, bool INV>
-    __device__ __forceinline__ void apply(C* u, int k, int j) const {
-        static_for<R - 1>([&](auto rc) {
-            constexpr int r = decltype(rc)::value + 1;
-            C t;
-            if constexpr (Ns * R == PlanOf<N>::N) {
-                t = w[k * (R - 1) + r - 1];
-            } else {
-                const int i = TwOff + (r - 1) * Ns + j;
-                t = mk<C>(table[i].x, table[i].y);
-            }
-            u[r] = INV ? cmulc(u[r], t) : cmul(u[r], t);
-        });
-    }
-};
-
-template <int N, class C>
-struct Twiddles<N, C, TW_SPLIT> {
-    static constexpr int COUNT = TwPowCountOf<N, RadicesOf<N>>::value > 0 ? 6 * TwPowCountOf<N, RadicesOf<N>>::value : 1;
-    C w[COUNT];  // group g: w[6 g .. 6 g + 2] = w^1..w^3, w[6 g + 3 .. 6 g + 5] = w^4, w^8, w^12
-    __device__ __forceinline__ void launder() {}
-    template <int TwOff, int RegOff, int PowOff, int R, int Ns, bool INV>
-    __device__ __forceinline__ void apply(C* u, int k, int) const {
-        static_assert(R == 16, "TW_SPLIT serves radix-16 passes");
-        const int g = 6 * (PowOff + k);
-        static_for<R - 1>([&](auto rc) {
-            constexpr int r = decltype(rc)::value + 1;
-            constexpr int a = r / 4, b = r % 4;
-            C t;
-            if constexpr (a == 0)
-                t = w[g + b - 1];
-            else if constexpr (b == 0)
-                t = w[g + 2 + a];
-            else
-                t = cmul(w[g + 2 + a], w[g + b - 1]);
-            u[r] = INV ? cmulc(u[r], t) : cmul(u[r], t);
-        });
-    }
-};
-
 template <int N, class C, int MODE, int E, int Ns, int TwOff, int RegOff, int PowOff, int R, int... Rest>
 __device__ __forceinline__ void load_twiddles_pass(Twiddles<N, C, MODE>& tw, int t, const C* __restrict__ table) {
     constexpr int T = PlanOf<N>::T;  // N is the plan key here
@@ -550,29 +391,10 @@ __device__ __forceinline__ void load_twiddles_pass(Twiddles<N, C, MODE>& tw, int
         static_for<NB>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
             const int j = (t + k * T) % Ns;
-            if constexpr (MODE == TW_CACHED) {
-                static_for<R - 1>([&](auto rc) {
-                    constexpr int r = decltype(rc)::value;
-                    tw.w[RegOff + k * (R - 1) + r] = table[TwOff + r * Ns + j];
-                });
-            } else if constexpr (MODE == TW_SPLIT) {
-                static_assert(R == 16, "TW_SPLIT serves radix-16 passes");
-                const int g = 6 * (PowOff + k);
-                static_for<3>([&](auto bc) {
-                    constexpr int b = decltype(bc)::value + 1;
-                    tw.w[g + b - 1] = table[TwOff + (b - 1) * Ns + j];      // w^b
-                    tw.w[g + 2 + b] = table[TwOff + (4 * b - 1) * Ns + j];  // w^(4b)
-                });
-            } else if constexpr (MODE == TW_LAST) {
-                if constexpr (sizeof...(Rest) == 0) {
-                    static_for<R - 1>([&](auto rc) {
-                        constexpr int r = decltype(rc)::value;
-                        tw.w[k * (R - 1) + r] = table[TwOff + r * Ns + j];
-                    });
-                }
-            } else {
-                tw.w1[PowOff + k] = table[TwOff + j];  // r = 1 entry
-            }
+            static_for<R - 1>([&](auto rc) {
+                constexpr int r = decltype(rc)::value;
+                tw.w[RegOff + k * (R - 1) + r] = table[TwOff + r * Ns + j];
+            });
         });
     }
     if constexpr (sizeof...(Rest) > 0) {
@@ -588,7 +410,7 @@ __device__ __forceinline__ void load_twiddles_impl(Twiddles<N, C, MODE>& tw, int
 }
 template <int N, class C, int MODE>
 __device__ __forceinline__ void load_twiddles(Twiddles<N, C, MODE>& tw, int t, const void* table) {
-    if constexpr (MODE == TW_DIRECT || MODE == TW_LAST)
+    if constexpr (MODE == TW_DIRECT)
         tw.table = (typename Twiddles<N, C, MODE>::GlobalPtr)table;
     if constexpr (MODE != TW_DIRECT)
         load_twiddles_impl<N, C, MODE>(tw, t, static_cast<const C*>(table), RadicesOf<N>{});
@@ -653,12 +475,6 @@ __device__ __forceinline__ void exchange_done(const Lds& lds) {
 // run that first pass in registers too (fft_pair): the projection between an
 // inverse and a forward transform then never rounds to complex64.
 // ------------------------------------------------------------------------
-#ifndef SLM_FUSE_PAIR
-#define SLM_FUSE_PAIR 1
-#endif
-#ifndef SLM_GROUP_FENCE
-#define SLM_GROUP_FENCE 1
-#endif
 
 template <class To, class From>
 __device__ __forceinline__ To cv(From a) {
@@ -695,11 +511,9 @@ __device__ __forceinline__ void stockham_from(V (&v)[L][E], int t, const Tw& tw,
                 });
             }
         });
-#if SLM_GROUP_FENCE
         // keep butterfly groups apart in the schedule: bounds the live registers
         // to about one group's worth (per line) in the compute type
         __builtin_amdgcn_sched_barrier(0);
-#endif
     });
     if constexpr (sizeof...(Rest) > 0) {
         exchange_sync(lds);
@@ -809,7 +623,7 @@ __device__ __forceinline__ void fft_pair(V (&v)[L][PlanOf<K>::E], int t, const T
     constexpr int T = PlanOf<K>::T;
     constexpr int R0 = first_radix(RadicesOf<K>{});
     constexpr int RL = last_radix(RadicesOf<K>{});
-    if constexpr (SLM_FUSE_PAIR && R0 == RL && kPlans[K].npass > 1) {
+    if constexpr (R0 == RL && kPlans[K].npass > 1) {
         // group k of the last pass is group k of the next transform's first pass
         auto sink = [&](auto lc, auto kc, auto& u) {
             constexpr int l = decltype(lc)::value;

@@ -137,57 +137,44 @@ enum Precision : int { PREC_F32 = 0, PREC_F64 = 1, PREC_NUM = 2 };
 // Workgroups of both passes keep their LDS at <= 80 KiB where the line allows,
 // so two of them share a CU and one's loads overlap the other's transforms.
 constexpr int kLdsPair = 80 * 1024;
-#ifndef SLM_ROW_PAIRS
-#define SLM_ROW_PAIRS 0  // measured equal at 4096 (row quads kept: whole 128-B lines)
-#endif
 
 // Lines per thread. A thread may carry L = 2 rows (row kernels) or columns
 // (column kernels) of the same tile: both lines share the thread's twiddles
 // (cached in registers), its exchange barriers and its address arithmetic, and
 // the two columns of a column tile are one 16-B access. Used for the narrow
-// column plans of SLM_COL_LINES2_MIN_N and longer: one column per thread in
+// column plans of kColLines2MinN and longer: one column per thread in
 // 8-wave workgroups could not hold a twiddle cache there (the 4096 column pass
 // had fallen back to table reads inside every pass).
-#ifndef SLM_COL_LINES2_MIN_N
-#define SLM_COL_LINES2_MIN_N 4096  // 4096: col pass 715 -> 626 us for 8 x 4096^2 (twiddles cached again)
-#endif
+constexpr int kColLines2MinN = 4096;  // 4096: col pass 715 -> 626 us for 8 x 4096^2 (twiddles cached again)
 // Rows: two adjacent rows per thread of the float32 4096 narrow plan, their
 // pieces of each 128-B line loaded and stored back to back (slot-major): the
 // 8 x 4096^2 row pass 789-806 -> 688 us, 1 x 4096^2 neutral, phases bitwise
 // equal (profiles/r04/ab_rows_l2_s6.txt; 228 VGPRs, two workgroups per CU).
 // Float64 rows keep one row per thread (290 VGPRs with two: one wave per SIMD).
-#ifndef SLM_ROW_LINES2_MIN_N
-#define SLM_ROW_LINES2_MIN_N 4096
-#endif
+constexpr int kRowLines2MinN = 4096;
 // Wave-local exchanges: where every thread of a line sits in one wave, a
 // Stockham exchange needs no workgroup barrier -- LDS writes, s_waitcnt, LDS
 // reads (fft_core.hpp, exchange_sync). That holds with the default lane maps
-// for rows of T <= 16 threads and for column tiles of T x CW / L <= 64 threads
-// (SLM_WAVE_LOCAL); rows of T = 32 are remapped so each row is one half-wave
-// (SLM_WAVE_LINE, T consecutive lanes per row). Measured per launch (f32,
+// for rows of T <= 16 threads and for column tiles of T x CW / L <= 64 threads;
+// rows of T = 32 are remapped so each row is one half-wave (T consecutive
+// lanes per row). Measured per launch (f32,
 // tools/kt.py, gpurun_out/s6): rows 256^2 x 64 15.66 -> 14.33 us, one 256^2
 // 4.24 -> 3.98 us, 16 x 512^2 23.45 -> 22.95 us; remapping rows of T = 64
 // (1024 wide) was slower (64 x 1024^2 260 -> 276 us), and so was remapping
 // columns to one column per wave (64 x 1024^2 265 -> 567 us: a wave then reads
 // 8 B per lane at a 32-B stride), so neither is done.
-#ifndef SLM_WAVE_LOCAL
-#define SLM_WAVE_LOCAL 1
-#endif
-#ifndef SLM_WAVE_LINE
-#define SLM_WAVE_LINE 1
-#endif
 template <int K>
 constexpr bool row_wave_remap(int lines_per_thread) {
-    return SLM_WAVE_LOCAL && SLM_WAVE_LINE && lines_per_thread == 1 && PlanOf<K>::T == 32;
+    return lines_per_thread == 1 && PlanOf<K>::T == 32;
 }
 template <int K>
 constexpr bool row_wave_local(int lines_per_thread) {
-    return SLM_WAVE_LOCAL && lines_per_thread == 1 && (PlanOf<K>::T <= 16 || row_wave_remap<K>(lines_per_thread));
+    return lines_per_thread == 1 && (PlanOf<K>::T <= 16 || row_wave_remap<K>(lines_per_thread));
 }
 
 template <int K, bool COL, int P = PREC_F32>
 constexpr int lines_of() {
-    return (kPlans[K].variant == 1 && PlanOf<K>::N >= (COL ? SLM_COL_LINES2_MIN_N : SLM_ROW_LINES2_MIN_N) &&
+    return (kPlans[K].variant == 1 && PlanOf<K>::N >= (COL ? kColLines2MinN : kRowLines2MinN) &&
             (COL || P == PREC_F32))
                ? 2
                : 1;
@@ -203,17 +190,13 @@ struct RowCfg {
     // half of each 128-B line, is placed on the same XCD: row_kernel remap)
     // Narrow plans (single small images: few workgroups per CU) always use
     // pairs: twice the workgroups, measured 11.6 -> 9.1 us per 1024^2 row pass.
-    static constexpr bool kPairs = (4 * PlanOf<K>::ROWSTRIDE * 8 > kLdsPair && (SLM_ROW_PAIRS || T >= 256)) ||
+    static constexpr bool kPairs = (4 * PlanOf<K>::ROWSTRIDE * 8 > kLdsPair && T >= 256) ||
                                    kPlans[K].variant == 1;
     // 4096 narrow rows with one row per thread run one row per workgroup: two
     // workgroups of 4 waves per CU instead of one of 8 (8 x 4096^2 row pass
     // 931 -> 755 us with write-back stores)
     static constexpr bool kSingle = kPlans[K].variant == 1 && PlanOf<K>::N >= 4096 && L == 1;
-#ifdef SLM_ROW_RPW
-    static constexpr int RPW = (T >= 64) ? SLM_ROW_RPW : 256 / T;
-#else
     static constexpr int RPW = (T >= 64) ? (kSingle ? 1 : kPairs ? 2 : 4) : 256 / T;
-#endif
     static_assert(RPW % L == 0, "rows per workgroup must be a multiple of the rows per thread");
     static constexpr bool kWave = row_wave_local<K>(L);    // each row inside one wave (wave-local exchanges)
     static constexpr bool kRemap = row_wave_remap<K>(L);   // ... by T consecutive lanes per row
@@ -227,7 +210,7 @@ struct ColCfg {
     static constexpr int T = PlanOf<K>::T;
     static constexpr int L = (CW % 2 == 0) ? lines_of<K, true>() : 1;  // columns per thread
     static constexpr int THREADS = (CW / L) * T;
-    static constexpr bool kWave = SLM_WAVE_LOCAL && T * (CW / L) <= 64;  // each column inside one wave
+    static constexpr bool kWave = T * (CW / L) <= 64;  // each column inside one wave
     static constexpr bool kValid =
         THREADS >= 64 && THREADS <= 1024 && lds_line(PlanOf<K>::N) * CW * 8 <= 160 * 1024;
 };
@@ -276,26 +259,10 @@ __device__ __forceinline__ void trace_entry(unsigned long long* tr) {
 #endif
 }
 
-// Waves per SIMD that the LDS footprint of a workgroup allows, handed to the
-// compiler as amdgpu_waves_per_eu (second __launch_bounds__ argument) so that
-// register allocation does not cap occupancy below what LDS permits (e.g. the
-// batched 1024 tiles: 35 KB of LDS would allow four workgroups per CU, but 150-200
-// VGPRs held them to two). Capped at SLM_MAX_WPE (4 => <= 128 VGPRs).
-#ifndef SLM_OCC
-#define SLM_OCC 0  // measured: the forced 128-VGPR cap spills the float64 transforms (slower everywhere)
-#endif
-#ifndef SLM_MAX_WPE
-#define SLM_MAX_WPE 4
-#endif
-constexpr int occupancy_wpe(int threads, long long lds_bytes) {
-    const int waves = (threads + 63) / 64;
-    long long wgs = lds_bytes > 0 ? (160LL * 1024) / lds_bytes : 64;
-    if (wgs < 1) wgs = 1;
-    long long wpe = wgs * waves / 4;
-    if (wpe < 1) wpe = 1;
-    if (wpe > SLM_MAX_WPE) wpe = SLM_MAX_WPE;
-    return SLM_OCC ? (int)wpe : 1;
-}
+// Kernels declare no waves-per-SIMD floor (__launch_bounds__(threads, 1)):
+// forcing the register budget to what LDS would allow (e.g. 128 VGPRs for
+// four workgroups of the batched 1024 tiles) spilled the float64 transforms
+// and was slower everywhere (r02).
 
 // Internal layout of the iteration state (X, Y, GD field, device target):
 // 4-column blocks, [x / 4][y][x % 4]. A 4-column panel is one contiguous run
@@ -306,13 +273,10 @@ constexpr int occupancy_wpe(int threads, long long lds_bytes) {
 // output, the column pass's input, and the target) and Y (the column pass's
 // output, the row pass's input, and the GD field) are [x / P][y][x % P] with
 // their own panel widths P: a column tile reads / writes whole panels of the
-// narrower layout, a row tile whole chunks of the wider one.
-#ifndef SLM_PANEL_X_LOG2
-#define SLM_PANEL_X_LOG2 2
-#endif
-#ifndef SLM_PANEL_Y_LOG2
-#define SLM_PANEL_Y_LOG2 2
-#endif
+// narrower layout, a row tile whole chunks of the wider one. The default pair
+// is 4-wide both ways (kPanelLog2); wider X or Y panels at 4096 trade the row
+// pass against the column pass.
+constexpr int kPanelLog2 = 2;
 // Layout pairs, chosen per plan (slm_plan_create): 0 = the default panels;
 // 1 = 8-wide X / 2-wide Y for single 1024^2 images on the narrow plan (2-column
 // tiles write whole Y panels, row pairs write 128-B X chunks: 1024^2 GS
@@ -321,11 +285,11 @@ constexpr int occupancy_wpe(int threads, long long lds_bytes) {
 enum LayoutId : int { LAYOUT_DEFAULT = 0, LAYOUT_NARROW = 1, kNumLayouts = 2 };
 template <int LID>
 struct LayoutOf {
-    static constexpr int X = LID == LAYOUT_NARROW ? 3 : SLM_PANEL_X_LOG2;
-    static constexpr int Y = LID == LAYOUT_NARROW ? 1 : SLM_PANEL_Y_LOG2;
+    static constexpr int X = LID == LAYOUT_NARROW ? 3 : kPanelLog2;
+    static constexpr int Y = LID == LAYOUT_NARROW ? 1 : kPanelLog2;
 };
-__host__ __device__ constexpr int layout_x_log2(int lid) { return lid == LAYOUT_NARROW ? 3 : SLM_PANEL_X_LOG2; }
-__host__ __device__ constexpr int layout_y_log2(int lid) { return lid == LAYOUT_NARROW ? 1 : SLM_PANEL_Y_LOG2; }
+__host__ __device__ constexpr int layout_x_log2(int lid) { return lid == LAYOUT_NARROW ? 3 : kPanelLog2; }
+__host__ __device__ constexpr int layout_y_log2(int lid) { return lid == LAYOUT_NARROW ? 1 : kPanelLog2; }
 // plans instantiated with the narrow layout pair (plan key 11: 1024 = 8.4.4.8)
 template <int K>
 constexpr bool kHasNarrowLayout = (K == 11);
@@ -407,12 +371,8 @@ __device__ __forceinline__ void store_field(float2* dst, float2 v, int wt) {
 // not hide it -- the last arrivals trail the first by several microseconds.
 constexpr unsigned long long kUnset = ~0ull;
 
-#ifndef SLM_GRID_SPIN_MAX
-#define SLM_GRID_SPIN_MAX (1 << 21)
-#endif
-#ifndef SLM_GRID_SLEEP
-#define SLM_GRID_SLEEP 8
-#endif
+constexpr int kGridSpinMax = 1 << 21;
+constexpr int kGridSleep = 8;
 __device__ __forceinline__ void store_coherent(double* dst, double v) {
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(dst), __builtin_bit_cast(unsigned long long, v),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -422,57 +382,26 @@ __device__ __forceinline__ double load_coherent(const double* src) {
                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
-#ifndef SLM_PREFETCH
-#define SLM_PREFETCH 0  // measured: no gain over one tile per workgroup (the transforms, not the loads, bound a tile)
-#endif
-// Persistent (looping, prefetching) kernels: float32 compute with at most 16
-// elements per thread, where the next tile's complex64 slots fit in registers
-// beside the current ones (-DSLM_PREFETCH=1 builds; twiddles as for one tile).
-// Every other kernel runs one tile per workgroup (grid = tiles). The host
-// sizes grids with the same predicate (slm_capi.hip, tile_grid).
-__host__ __device__ constexpr bool tile_persistent(int prec, int e) {
-    return SLM_PREFETCH && prec == PREC_F32 && e <= 16;
-}
-
 template <int P>
 using CplxOf = std::conditional_t<P == 0, float2, double2>;
 
-// exchange in the compute type when that keeps the workgroup's LDS <= 80 KiB
-// (two workgroups per CU), otherwise in complex64
-#ifndef SLM_F64_XCHG
-#define SLM_F64_XCHG 0
-#endif
-#ifndef SLM_F64_TW
-#define SLM_F64_TW TW_DIRECT
-#endif
-// float64 exchanges: narrow plans (more passes, hence more exchange roundings,
-// used for single small images where LDS is plentiful) and SLM_F64_XCHG builds
-// Narrow plans up to this length exchange in float64. Longer ones exchange in
-// complex64: half the LDS traffic, measured -2.5 % (1024^2) / -9 % (768x1024)
-// per iteration for warm-start parity 1.2e-6 instead of 4.3e-7 at 1024^2.
-#ifndef SLM_NARROW_F64_XCHG_MAX
-#define SLM_NARROW_F64_XCHG_MAX 512
-#endif
+// Exchange type of float64 butterflies: float64 for narrow plans up to
+// kNarrowF64XchgMax (more passes, hence more exchange roundings; single small
+// images, where LDS is plentiful) while the workgroup's LDS stays <= 80 KiB,
+// complex64 otherwise: half the LDS traffic, measured -2.5 % (1024^2) / -9 %
+// (768x1024) per iteration for warm-start parity 1.2e-6 instead of 4.3e-7 at
+// 1024^2.
+constexpr int kNarrowF64XchgMax = 512;
 template <int P, long long SLOTS, int K>
-using XchgOf = std::conditional_t<((SLM_F64_XCHG || (kPlans[K].variant == 1 && kPlans[K].n <= SLM_NARROW_F64_XCHG_MAX)) &&
-                                   P == 1 && SLOTS * 16 <= 80 * 1024),
+using XchgOf = std::conditional_t<((kPlans[K].variant == 1 && kPlans[K].n <= kNarrowF64XchgMax) && P == 1 &&
+                                   SLOTS * 16 <= 80 * 1024),
                                   double2, float2>;
 
-// float64: every twiddle of the thread cached in registers (loaded once per
-// kernel, behind the field loads, shared by both transforms) when they fit in
-// SLM_F64_TWCACHE_MAX VGPRs (the narrow single-image plans), so no pass waits
-// on a table load; otherwise read where used.
-#ifndef SLM_F64_TWCACHE_MAX
-#define SLM_F64_TWCACHE_MAX 0  // measured neutral at 1024^2 (80 caches the narrow plans)
-#endif
+// float64 butterflies read their twiddles from the table where used (caching
+// them in registers measured neutral at 1024^2).
 template <int P, int THREADS, int K, bool COL, int L = 1>
 constexpr int tw_mode() {
-    if constexpr (P == 1)
-        return TwCountOf<K, RadicesOf<K>>::value * 4 <= SLM_F64_TWCACHE_MAX && THREADS <= 512 ? TW_CACHED
-                                                                                             : SLM_F64_TW;
-#ifdef SLM_F32_TW
-    return SLM_F32_TW;
-#else
+    if constexpr (P == 1) return TW_DIRECT;
     // float32 (measured per launch):
     //  * column kernels of 2048+ lines read the table where used (4096:
     //    156 -> 127 us, 2048: 109 -> 93 us; registers 208 -> 122, two
@@ -481,15 +410,8 @@ constexpr int tw_mode() {
     //    form w^2.. from w^1 ran 7-10 % faster at 2048/4096 but took the 4096^2
     //    warm-start parity from 3.1e-6 to 1.3e-5 rms after 100 iterations.)
     //  * two-column threads (L = 2) cache them again: one cache serves both lines
-#ifdef SLM_F32_COL_TW
-    if constexpr (COL) return SLM_F32_COL_TW;
-#endif
     if constexpr (COL && PlanOf<K>::N >= 2048 && L == 1) return TW_DIRECT;
-#ifdef SLM_F32_ROW_TW
-    if constexpr (!COL) return SLM_F32_ROW_TW;
-#endif
     return THREADS <= 512 && PlanOf<K>::E <= 16 ? TW_CACHED : TW_DIRECT;
-#endif
 }
 
 template <int TT>
@@ -537,17 +459,14 @@ struct TgtLoad<TGT_AMP> {
     __device__ __forceinline__ static float intensity(float a) { return a * a; }
 };
 
-// Wave reductions of doubles without the LDS pipe (-DSLM_DPP_REDUCE=0: __shfl_xor
-// through ds_bpermute; measured GD 1024^2 fused column pass 13.3 -> 12.4 us, the
+// Wave reductions of doubles without the LDS pipe (instead of __shfl_xor
+// through ds_bpermute: measured GD 1024^2 fused column pass 13.3 -> 12.4 us, the
 // statistics and the barrier fold sit before and inside its grid wait):
 // within each 16-lane row a rotation by 4 then by 8 folds each residue class
 // mod 4 (whichever way DPP row_ror turns), two quad_perm steps fold the quad;
 // v_permlane16_swap / v_permlane32_swap of a value with itself then hand every
 // lane both rows / halves. Every lane ends with the wave total (the lanes'
 // association orders differ; thread 0's value is the one used).
-#ifndef SLM_DPP_REDUCE
-#define SLM_DPP_REDUCE 1
-#endif
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double x) {
     const unsigned long long b = __builtin_bit_cast(unsigned long long, x);
@@ -586,17 +505,9 @@ template <int THREADS>
 __device__ __forceinline__ void block_reduce_stats(double& mx, double& s2, double& st) {
     constexpr int NW = (THREADS + 63) / 64;
     __shared__ double red[NW][3];
-#if SLM_DPP_REDUCE
     mx = wave_fold<true>(mx);
     s2 = wave_fold<false>(s2);
     st = wave_fold<false>(st);
-#else
-    for (int off = 32; off > 0; off >>= 1) {
-        mx = fmax(mx, __shfl_xor(mx, off));
-        s2 += __shfl_xor(s2, off);
-        st += __shfl_xor(st, off);
-    }
-#endif
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     if (NW > 1) {
         if (lane == 0) {
@@ -620,11 +531,7 @@ template <int THREADS>
 __device__ __forceinline__ void block_reduce_max(double& mx) {
     constexpr int NW = (THREADS + 63) / 64;
     __shared__ double redm[NW];
-#if SLM_DPP_REDUCE
     mx = wave_fold<true>(mx);
-#else
-    for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));
-#endif
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     if (NW > 1) {
         if (lane == 0) redm[wid] = mx;
@@ -647,8 +554,8 @@ __device__ __forceinline__ double wait_set(const double* src, int* fault) {
     int spins = 0;
     while ((v = load_coherent_bits(src)) == kUnset) {
         if ((spins & 63) == 0 && __hip_atomic_load(fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return 0.0;
-        __builtin_amdgcn_s_sleep(SLM_GRID_SLEEP);
-        if (++spins > SLM_GRID_SPIN_MAX) {
+        __builtin_amdgcn_s_sleep(kGridSleep);
+        if (++spins > kGridSpinMax) {
             __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return 0.0;
         }
@@ -700,39 +607,18 @@ __device__ __forceinline__ void sgpr_pin(const A&... a) {
 }
 
 // ------------------------------------------------------------------------
-// persistent tile loop (both passes)
+// tile of a workgroup (both passes)
 // ------------------------------------------------------------------------
-// A launch covers `total` tiles (column panels or row groups of every
-// hologram) with G = gridDim.x <= total workgroups, G at most what the chip
-// holds at once (host: tile_grid). Workgroup w takes tiles lid(w), lid(w) + G,
-// ... where lid is the XCD-aware remap, so within one round the workgroups of
-// an XCD hold neighbouring tiles. The next tile's inputs are loaded into
-// registers before the current tile is transformed (kPrefetch), so their HBM
-// latency hides behind the transforms and the current tile's stores; the LDS
-// barriers never wait for vector memory (lds_barrier), so the loads stay in
-// flight across them.
-template <bool PERSIST, class LoadF, class ProcF, class VA, class TA>
+// One tile (column panel or row group of one hologram) per workgroup, grid =
+// tiles; the XCD-aware remap gives the workgroups of an XCD neighbouring
+// tiles. (A persistent loop prefetching the next tile's inputs into registers
+// measured neutral: the transforms, not the loads, bound a tile.)
+template <class LoadF, class ProcF, class VA, class TA>
 __device__ __forceinline__ void tile_loop(long long total, LoadF&& load, ProcF&& process, VA& v, TA& tv) {
-    const int G = gridDim.x;
-    long long tile = xcd_remap(blockIdx.x, G);
+    const long long tile = xcd_remap(blockIdx.x, gridDim.x);
     if (tile >= total) return;
     load(tile, v, tv);
-    if constexpr (!PERSIST) {
-        process(tile, v, tv);
-    } else {
-        for (;;) {
-            const long long next = tile + G;
-            const bool more = next < total;
-            VA vn;
-            TA tn;
-            if (more) load(next, vn, tn);
-            process(tile, v, tv);
-            if (!more) break;
-            __builtin_memcpy(&v, &vn, sizeof(VA));
-            __builtin_memcpy(&tv, &tn, sizeof(TA));
-            tile = next;
-        }
-    }
+    process(tile, v, tv);
 }
 
 // ------------------------------------------------------------------------
@@ -741,45 +627,24 @@ __device__ __forceinline__ void tile_loop(long long total, LoadF&& load, ProcF&&
 // Double-buffered LDS exchanges (fft_core.hpp, LdsLine / LdsTile ALT): one
 // barrier per exchange instead of two, for twice the exchange LDS. Used where
 // the second buffer leaves the workgroups per CU the launch gets unchanged.
-#ifndef SLM_LDS_DOUBLE
-#define SLM_LDS_DOUBLE 1
-#endif
 // Measured: 1024^2 GS 18.3 -> 17.8 us of kernels per iteration; the 4096 rows
 // (2 x 34 KB per one-row workgroup still fits the two workgroups their VGPRs
 // allow) gained nothing (8 x 4096^2 row pass 799 -> 795 us, one image
 // 100 -> 105 us), and 4096 columns would drop to one workgroup per CU.
 template <int K, bool COL>
-constexpr bool kLdsDouble = SLM_LDS_DOUBLE && K == 11;
+constexpr bool kLdsDouble = K == 11;
 
 // Wave-shuffle transform pair (fft_shuffle.hpp) for the float32 GS iteration
 // on 1024-point narrow lines (plan key 11, the headline 1024^2 image): two of
-// the pair's six exchanges go through LDS, four are v_permlane swaps.
-// -DSLM_SHUFFLE=0 keeps the Stockham pair there (A/B builds).
-#ifndef SLM_SHUFFLE
-#define SLM_SHUFFLE 1
-#endif
-#ifndef SLM_SHUFFLE4096
-#define SLM_SHUFFLE4096 0  // A/B knob: the wave-shuffle pair for 4096-point GS rows
-#endif
+// the pair's six exchanges go through LDS, four are v_permlane swaps. (A
+// 4096-point shuffle pair for the float32 rows measured slower, 862 against
+// 788 us per 8 x 4096^2 row pass, and failed the float32 +100 gate at 1.02e-5:
+// profiles/r04/ab_shuf4096_s1.txt.)
 template <int K, int P>
-constexpr bool kShuffle4096 = SLM_SHUFFLE4096 && P == PREC_F32 && PlanOf<K>::N == kShuf4N && PlanOf<K>::E == 16;
-template <int K, int P>
-constexpr bool kShuffle = SLM_SHUFFLE && P == PREC_F32 && PlanOf<K>::N == kShufN && PlanOf<K>::E == 8;
-
-template <int K, int P>
-constexpr int row_wpe() {
-    using X = XchgOf<P, (long long)RowCfg<K, P>::RPW * PlanOf<K>::ROWSTRIDE, K>;
-    // per-plan waves-per-SIMD floor for the float32 row kernels (register budget
-    // 512 / w; A/B knob: -DSLM_ROW_WPE_K=<key> -DSLM_ROW_WPE=<w>)
-#if defined(SLM_ROW_WPE_K) && defined(SLM_ROW_WPE)
-    if constexpr (K == SLM_ROW_WPE_K && P == 0) return SLM_ROW_WPE;
-#endif
-    return occupancy_wpe(RowCfg<K, P>::THREADS,
-                         (kLdsDouble<K, false> ? 2 : 1) * (long long)RowCfg<K, P>::RPW * PlanOf<K>::ROWSTRIDE * sizeof(X));
-}
+constexpr bool kShuffle = P == PREC_F32 && PlanOf<K>::N == kShufN && PlanOf<K>::E == 8;
 
 template <int K, int MODE, int P, int LID>
-__global__ void __launch_bounds__((RowCfg<K, P>::THREADS), (row_wpe<K, P>())) row_kernel(RowParams p) {
+__global__ void __launch_bounds__((RowCfg<K, P>::THREADS), 1) row_kernel(RowParams p) {
     constexpr int LAYOUT_X = LayoutOf<LID>::X, LAYOUT_Y = LayoutOf<LID>::Y;
     using C = CplxOf<P>;
     using S = Scalar<C>;
@@ -793,11 +658,8 @@ __global__ void __launch_bounds__((RowCfg<K, P>::THREADS), (row_wpe<K, P>())) ro
     using X = XchgOf<P, (long long)RPW * LINE, K>;
     using V = StateOf<P, X>;
     constexpr int ALT = kLdsDouble<K, false> ? RPW * LINE : 0;
-    // wave-shuffle pair for 4096-point rows (fft_shuffle.hpp; float32 GS, one row per workgroup)
-    constexpr bool SHUF4 = kShuffle4096<K, P> && MODE == ROW_GS_MAIN && RPW == 1 && L == 1 &&
-                           RowCfg<K, P>::THREADS == 256 && std::is_same_v<X, float2>;
     constexpr int SMEM_ROW = (ALT ? 2 : 1) * RPW * LINE;
-    __shared__ X smem[SHUF4 && SMEM_ROW < 2 * kShuf4N ? 2 * kShuf4N : SMEM_ROW];
+    __shared__ X smem[SMEM_ROW];
 
     // lane -> (row group within the quad, transform thread t): TL consecutive
     // t of one row group, then the next group of the quad. One wave instruction
@@ -832,11 +694,8 @@ __global__ void __launch_bounds__((RowCfg<K, P>::THREADS), (row_wpe<K, P>())) ro
     static_assert(!SHUF || (std::is_same_v<X, float2> && sizeof(smem) >= 4 * kShufN * sizeof(float2)),
                   "the shuffle pair needs two 2-line complex64 exchange buffers");
     ShuffleTw stw;
-    ShuffleTw4096 stw4;
     if constexpr (SHUF)
         load_shuffle_tw(stw, threadIdx.x, static_cast<const float2*>(p.tw) + twiddle_count_key(K));
-    else if constexpr (SHUF4)
-        load_shuffle4096_tw(stw4, threadIdx.x, static_cast<const float2*>(p.tw) + twiddle_count_key(K));
     else
         load_twiddles<K, C>(tw, t, p.tw);
 
@@ -911,15 +770,7 @@ __global__ void __launch_bounds__((RowCfg<K, P>::THREADS), (row_wpe<K, P>())) ro
         } else if constexpr (MODE == ROW_GS_MAIN) {
             // A -> B = a_in A/|A| (src/algorithms.py:30)
             auto epi = [&](int l, int m, C& z) { z = unit_scale(z, ain_at(l, m)); };
-            if constexpr (SHUF4) {
-                // the pair's middle holds element shuffle4096_klow(tid) + 256 m
-                const int km = shuffle4096_klow(threadIdx.x);
-                shuffle4096_pair<true, false>(v[0], threadIdx.x, stw4, reinterpret_cast<float2*>(smem),
-                                              [&](int, int m, C& z) {
-                                                  const S a = p.ain ? (S)p.ain[roff + km + T * m] : (S)1;
-                                                  z = unit_scale(z, a);
-                                              });
-            } else if constexpr (SHUF)
+            if constexpr (SHUF)
                 shuffle_pair<true, false>(v[0], threadIdx.x, stw, reinterpret_cast<float2*>(smem), epi);
             else
                 fft_pair<K, true, false, C>(v, t, tw, lds, epi);
@@ -1033,7 +884,7 @@ __global__ void __launch_bounds__((RowCfg<K, P>::THREADS), (row_wpe<K, P>())) ro
     };
     V v[L][E];
     float none[1];
-    tile_loop<tile_persistent(P, E)>(p.ntile * (long long)p.B, load, process, v, none);
+    tile_loop(p.ntile * (long long)p.B, load, process, v, none);
 }
 
 // ------------------------------------------------------------------------
@@ -1102,7 +953,7 @@ __device__ __forceinline__ void gd_inverse_pair(V (&wu)[L][E], V (&wv)[L][E], in
 // touches one line only, and the interleave's stride-2 slots cost 4 / 2 extra
 // cycles per write / read (tools/lds_banks.py).
 template <int K, int CW>
-constexpr bool kColLineMajor = SLM_COL_LINE_MAJOR && ColCfg<K, CW>::L == CW;
+constexpr bool kColLineMajor = ColCfg<K, CW>::L == CW;
 
 template <int K, int CW, int P, int MODE>
 constexpr bool kColDualInv() {
@@ -1115,18 +966,8 @@ constexpr int col_lds_width() {
     return kColDualInv<K, CW, P, MODE>() ? 2 * CW : CW;
 }
 
-template <int K, int CW, int P, int MODE = COL_GS_MAIN>
-constexpr int col_wpe() {
-    using X = XchgOf<P, (long long)PlanOf<K>::LINE * CW, K>;
-#if defined(SLM_COL_WPE_K) && defined(SLM_COL_WPE)
-    if constexpr (K == SLM_COL_WPE_K && P == 0) return SLM_COL_WPE;
-#endif
-    return occupancy_wpe(ColCfg<K, CW>::THREADS, (kLdsDouble<K, true> ? 2 : 1) * (long long)PlanOf<K>::LINE *
-                                                     col_lds_width<K, CW, P, MODE>() * sizeof(X));
-}
-
 template <int K, int CW, int MODE, int TT, int P, int LID>
-__global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P, MODE>())) col_kernel(ColParams p) {
+__global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), 1) col_kernel(ColParams p) {
     constexpr int LAYOUT_X = LayoutOf<LID>::X, LAYOUT_Y = LayoutOf<LID>::Y;
     using C = CplxOf<P>;
     using S = Scalar<C>;
@@ -1470,7 +1311,7 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), (col_wpe<K, CW, P, M
     };
     V v[L][E];
     float tv[L][NT];
-    tile_loop<tile_persistent(P, E)>(p.nwg * (long long)p.B, load, process, v, tv);
+    tile_loop(p.nwg * (long long)p.B, load, process, v, tv);
 }
 
 // ------------------------------------------------------------------------

@@ -21,9 +21,7 @@ namespace {
 
 // waves per SIMD the register budget must allow: 4 = two 512-thread
 // workgroups per CU (<= 128 VGPRs), which their LDS (<= 72 KiB each) allows
-#ifndef MR_WPE
-#define MR_WPE 4
-#endif
+constexpr int kWavesPerSimd = 4;
 
 __device__ __forceinline__ double amp_of(const void* tgt, int tt, long long i) {
     if (tt == TGT_U8) return (double)TgtLoad<TGT_U8>::amp(TgtLoad<TGT_U8>::load(tgt, i));
@@ -47,7 +45,7 @@ __device__ __forceinline__ double2 u_of(double2 x, double a) {
 __device__ __forceinline__ double2 round_c64(double2 z) { return make_double2((double)(float)z.x, (double)(float)z.y); }
 
 template <int OP>
-__global__ void __launch_bounds__(kThreads, MR_WPE) mr_row_kernel(RowArgs a) {
+__global__ void __launch_bounds__(kThreads, kWavesPerSimd) mr_row_kernel(RowArgs a) {
     extern __shared__ double2 lds[];
     const int tiles = (a.H + a.rpw - 1) / a.rpw;
     const int b = blockIdx.x / tiles;
@@ -144,7 +142,7 @@ __global__ void __launch_bounds__(kThreads, MR_WPE) mr_row_kernel(RowArgs a) {
 }
 
 template <int OP>
-__global__ void __launch_bounds__(kThreads, MR_WPE) mr_col_kernel(ColArgs a) {
+__global__ void __launch_bounds__(kThreads, kWavesPerSimd) mr_col_kernel(ColArgs a) {
     extern __shared__ double2 lds[];
     const int b = blockIdx.x / a.nwg;
     const int tile = blockIdx.x - b * a.nwg;

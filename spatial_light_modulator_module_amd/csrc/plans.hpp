@@ -28,10 +28,7 @@ struct RadixPlan {
 // inverse and a forward transform runs inside one butterfly group
 // (fft_core.hpp, fft_pair).
 // 4096: 32 elements per thread in radix-8 passes (512-thread column tiles,
-// no float64 spills); -DSLM_PLAN4096 selects experimental variants
-#ifndef SLM_PLAN4096
-#define SLM_PLAN4096 {4096, 32, 0, 4, {8, 8, 8, 8}}
-#endif
+// no float64 spills)
 constexpr RadixPlan kPlans[] = {
     {64, 8, 0, 2, {8, 8, 0, 0}},
     {128, 16, 0, 3, {4, 8, 4, 0}},
@@ -40,7 +37,7 @@ constexpr RadixPlan kPlans[] = {
     {768, 24, 0, 3, {8, 12, 8, 0}},
     {1024, 16, 0, 3, {16, 4, 16, 0}},
     {2048, 16, 0, 3, {16, 8, 16, 0}},
-    SLM_PLAN4096,
+    {4096, 32, 0, 4, {8, 8, 8, 8}},
     {256, 8, 1, 3, {8, 4, 8, 0}},
     {512, 8, 1, 3, {8, 8, 8, 0}},
     {768, 12, 1, 4, {4, 12, 4, 4}},

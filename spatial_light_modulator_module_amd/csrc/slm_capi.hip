@@ -128,8 +128,8 @@ int get_twiddles(int pk, int prec, const void** out) {
         host.push_back(1.0);
         host.push_back(0.0);
     }
-    if ((pl.n == kShufN && pl.e == 8) || (pl.n == kShuf4N && pl.e == 16)) {
-        // the wave-shuffle pairs' table (fft_shuffle.hpp): the N roots
+    if (pl.n == kShufN && pl.e == 8) {
+        // the wave-shuffle pair's table (fft_shuffle.hpp): the N roots
         // exp(-2 pi i e / N), after the Stockham entries (twiddle_count_key)
         for (int e = 0; e < pl.n; ++e) {
             const double ang = -2.0 * M_PI * (double)e / (double)pl.n;
@@ -409,8 +409,7 @@ int pick_cw(int ck, int W) {
 // (e.g. a single 1024^2 hologram), else the wide one. $SLM_PLAN=wide|narrow
 // forces a variant where it exists.
 // Float32 transforms take the narrow plan where the wide one holds more than
-// 16 elements per thread (4096: 32): those are not persistent (kernels.hpp,
-// tile_persistent) and spill.
+// 16 elements per thread (4096: 32 spill).
 int pick_plan(int n, long long elems, int prec, bool row = false) {
     const int wide = plan_index(n, 0), narrow = plan_index(n, 1);
     if (narrow < 0) return wide;
@@ -548,35 +547,10 @@ ColParams col_params(slm_plan* p) {
 }
 
 
-// Grid of a persistent tile loop (kernels.hpp, tile_loop): as many workgroups
-// as the chip holds at once (occupancy query, cached per kernel), never more
-// than there are tiles. $SLM_PERSIST=0 launches one workgroup per tile.
-int tile_grid(const void* fn, int threads, long long tiles, bool persistent, int* grid) {
-    static std::mutex mu;  // slm_gs_multi creates plans from several host threads
-    std::lock_guard<std::mutex> lk(mu);
-    static std::map<const void*, int> resident;
-    static int cus = 0, persist = -1;
-    if (persist < 0) {
-        const char* s = std::getenv("SLM_PERSIST");
-        persist = s ? std::atoi(s) : 1;
-    }
+// One workgroup per tile (kernels.hpp, tile_loop).
+int tile_grid(long long tiles, int* grid) {
     if (tiles > INT_MAX) return fail(SLM_ERR_ARG, "%lld tiles exceed one launch", tiles);
-    if (!persist || !persistent) {
-        *grid = (int)tiles;
-        return 0;
-    }
-    if (!cus) {
-        int dev = 0;
-        HIP_TRY(hipGetDevice(&dev));
-        HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    }
-    auto it = resident.find(fn);
-    if (it == resident.end()) {
-        int per_cu = 0;
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, 0));
-        it = resident.emplace(fn, std::max(1, per_cu)).first;
-    }
-    *grid = (int)std::min<long long>(tiles, (long long)it->second * cus * persist);
+    *grid = (int)tiles;
     return 0;
 }
 
@@ -587,8 +561,7 @@ int launch_row(slm_plan* p, int mode, const RowParams& rp, int cls) {
     r.B = p->B;
     r.ntile = p->H / p->rpw;
     int grid = 0;
-    RC(tile_grid((const void*)fn, p->row_threads, (long long)r.ntile * p->B,
-                  tile_persistent(p->prec, kPlans[p->row_key].e), &grid));
+    RC(tile_grid((long long)r.ntile * p->B, &grid));
     return launch(p, cls, fn, dim3(grid), dim3(p->row_threads), r);
 }
 
@@ -599,8 +572,7 @@ int launch_col(slm_plan* p, int mode, const ColParams& cp, int cls) {
     ColParams c = cp;
     c.B = p->B;
     int grid = 0;
-    RC(tile_grid((const void*)fn, p->col_threads, (long long)p->nwg * p->B,
-                  tile_persistent(p->prec, kPlans[p->col_key].e), &grid));
+    RC(tile_grid((long long)p->nwg * p->B, &grid));
     return launch(p, cls, fn, dim3(grid), dim3(p->col_threads), c);
 }
 
@@ -698,7 +670,7 @@ int enqueue_gs(slm_plan* p, int loops, double tol, int checked) {
 // (occupancy x CUs, one tile per workgroup). Otherwise the statistics pass and
 // the gradient pass run as two launches. $SLM_GD_FUSE=0 forces two launches.
 ColFn gd_fused_fn(slm_plan* p, int checked) {
-    if (!p->gd_fuse || !p->gsync || checked || tile_persistent(p->prec, kPlans[p->col_key].e)) return nullptr;
+    if (!p->gd_fuse || !p->gsync || checked) return nullptr;
     if (p->gd_mode != GD_AUTO && p->gd_mode != GD_FUSED) return nullptr;
     if (2LL * p->B * p->max_loops * (1 + p->nwg) > INT_MAX) return nullptr;  // slot area: two launches instead
     ColFn fn = col_fn(p->col_key, p->cw, COL_GD_FUSED, p->tt, p->prec, p->lid);
@@ -1488,7 +1460,7 @@ int slm_plan_engine(slm_plan* p, int* col_engine, int* row_engine) {
         return 0;
     }
     auto shuf = [&](int key) {
-        return SLM_SHUFFLE && p->prec == PREC_F32 && key >= 0 && kPlans[key].n == kShufN && kPlans[key].e == 8;
+        return p->prec == PREC_F32 && key >= 0 && kPlans[key].n == kShufN && kPlans[key].e == 8;
     };
     *col_engine = shuf(p->col_key) && p->cw == 2 ? 1 : 0;
     *row_engine = shuf(p->row_key) && p->rpw == 2 ? 1 : 0;
