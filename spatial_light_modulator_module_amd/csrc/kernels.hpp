@@ -1354,113 +1354,5 @@ __device__ __forceinline__ void reduce_slab(const StatsParams& p, int b, int i, 
     }
 }
 
-#ifdef SLM_DEFINE_SMALL_KERNELS  // defined by exactly one translation unit (slm_capi.hip)
-__global__ void __launch_bounds__(256) stats_reduce_kernel(StatsParams p) {
-    const int i = blockIdx.x, b = blockIdx.y;
-    const int last = min(p.stop_iter[b], p.max_loops - 1);
-    if (i > last) return;
-    __shared__ double o[4];
-    reduce_slab(p, b, i, o);
-    if (threadIdx.x == 0)
-        for (int k = 0; k < 4; ++k) p.stats[((long long)b * p.max_loops + i) * 4 + k] = o[k];
-}
-
-// Tolerance check of one iteration (while error > tolerance, src/algorithms.py:29,83).
-__global__ void __launch_bounds__(256) stats_finalize_kernel(StatsParams p) {
-    const int b = blockIdx.x;
-    if (p.iter > p.stop_iter[b]) return;
-    __shared__ double o[4];
-    reduce_slab(p, b, p.iter, o);
-    if (threadIdx.x == 0) {
-        if (!(o[3] > p.tol)) p.stop_iter[b] = p.iter;
-    }
-}
-
-// hologram = np.angle(input) of the GD field (src/algorithms.py:111); the
-// field is in the blocked layout, the phase row-major.
-template <int PLOG>
-__global__ void __launch_bounds__(256) field_phase_kernel(const float2* field, float* phase, long long n, int H,
-                                                          int W) {
-    const long long holo = (long long)H * W;
-    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-        const long long b = i / holo, r = i - b * holo;
-        const int y = (int)(r / W), x = (int)(r - (long long)y * W);
-        const float2 f = field[b * holo + blk_index<PLOG>(y, x, H)];
-        phase[i] = atan2f(f.y, f.x);
-    }
-}
-
-// blocked layout -> row-major for float planes (the expected output), through
-// an LDS tile of 64 x 64: the reads are whole panel runs (64 rows x P floats
-// contiguous per panel), the writes 256-B row segments. grid (W / 64, H / 64,
-// B), 256 threads; H and W are multiples of 64 for every supported side.
-template <int PLOG>
-__global__ void __launch_bounds__(256) unblock_tile_kernel(const float* in, float* out, int H, int W) {
-    // 64 x 64 tiles; vector accesses both ways: panel rows in (VW = min(P, 4)
-    // floats per lane), 16-B row pieces out (sides are multiples of 64)
-    constexpr int P = 1 << PLOG;
-    constexpr int VW = P < 4 ? P : 4;
-    constexpr int LD = 68;  // row stride: 16-B aligned rows for ds_read_b128
-    __shared__ __attribute__((aligned(16))) float tile[64 * LD];
-    const long long holo = (long long)H * W;
-    const int x0 = blockIdx.x * 64, y0 = blockIdx.y * 64;
-    const float* src = in + blockIdx.z * holo;
-    float* dst = out + blockIdx.z * holo;
-#pragma unroll
-    for (int k = 0; k < 16 / VW; ++k) {
-        const int e = (threadIdx.x + 256 * k) * VW;  // panel-major order of the tile: (q, yy, xx)
-        const int xx = e & (P - 1), yy = (e >> PLOG) & 63, q = e >> (PLOG + 6);
-        const float* s0 = src + (((long long)(x0 >> PLOG) + q) * H + y0 + yy) * P + xx;
-        float* t0 = tile + yy * LD + q * P + xx;
-        if constexpr (VW == 4) {
-            const float4 v = *reinterpret_cast<const float4*>(s0);
-            t0[0] = v.x;
-            t0[1] = v.y;
-            t0[2] = v.z;
-            t0[3] = v.w;
-        } else {
-            const float2 v = *reinterpret_cast<const float2*>(s0);
-            t0[0] = v.x;
-            t0[1] = v.y;
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int i = threadIdx.x + 256 * k;
-        const int yy = i >> 4, xx = (i & 15) * 4;
-        *reinterpret_cast<float4*>(dst + (long long)(y0 + yy) * W + x0 + xx) =
-            *reinterpret_cast<const float4*>(tile + yy * LD + xx);
-    }
-}
-
-// float32 target (row-major) -> its amplitude sqrt(T) in the blocked layout
-// (GS plans keep a_T on the device: TGT_AMP), the square root of TgtLoad<TGT_F32>
-template <int PLOG>
-__global__ void __launch_bounds__(256) amp_blocked_kernel(const float* in, float* out, long long n, int H, int W) {
-    const long long holo = (long long)H * W;
-    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-        const long long b = i / holo, r = i - b * holo;
-        const int y = (int)(r / W), x = (int)(r - (long long)y * W);
-        out[b * holo + blk_index<PLOG>(y, x, H)] = TgtLoad<TGT_F32>::amp(in[i]);
-    }
-}
-
-// row-major <-> blocked layout (uploads, the FFT test entry)
-template <typename V, bool TO_BLOCKED, int PLOG>
-__global__ void __launch_bounds__(256) relayout_kernel(const V* in, V* out, long long n, int H, int W) {
-    const long long holo = (long long)H * W;
-    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-        const long long b = i / holo, r = i - b * holo;
-        const int y = (int)(r / W), x = (int)(r - (long long)y * W);
-        const long long j = b * holo + blk_index<PLOG>(y, x, H);
-        if (TO_BLOCKED)
-            out[j] = in[i];
-        else
-            out[i] = in[j];
-    }
-}
-
-#endif  // SLM_DEFINE_SMALL_KERNELS
 
 }  // namespace slm

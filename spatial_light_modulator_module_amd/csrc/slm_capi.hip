@@ -24,7 +24,7 @@
 #include "../../include/slm_hip.h"
 #include "dispatch.hpp"
 #include "generic.hpp"
-#define SLM_DEFINE_SMALL_KERNELS
+#include "layout_kernels.hpp"
 #include "kernels.hpp"
 
 using namespace slm;
@@ -249,8 +249,20 @@ __global__ void __launch_bounds__(kTsThreads) target_stats_final_kernel(const do
 
 // plog: panel width log2 of the destination / source blocked layout
 // (layout_x_log2(lid): X buffers, the target; layout_y_log2(lid): Y, the GD field)
+// float / complex64 planes of 64-multiple sides move through LDS tiles
+// (layout_kernels.hpp, tile_relayout_kernel), byte planes element-wise
 template <int PLOG, typename V>
 void relayout_launch(const V* in, V* out, long long n, int H, int W, bool to_blocked, hipStream_t st) {
+    if constexpr (sizeof(V) == 4 || sizeof(V) == 8) {
+        if (H % 64 == 0 && W % 64 == 0) {
+            const dim3 grid(W / 64, H / 64, (unsigned)(n / ((long long)H * W)));
+            if (to_blocked)
+                hipLaunchKernelGGL((tile_relayout_kernel<V, PLOG, true>), grid, dim3(256), 0, st, in, out, H, W);
+            else
+                hipLaunchKernelGGL((tile_relayout_kernel<V, PLOG, false>), grid, dim3(256), 0, st, in, out, H, W);
+            return;
+        }
+    }
     const int grid = (int)std::min<long long>(8192, (n + 255) / 256);
     if (to_blocked)
         hipLaunchKernelGGL((relayout_kernel<V, true, PLOG>), dim3(grid), dim3(256), 0, st, in, out, n, H, W);
@@ -581,10 +593,10 @@ int launch_col(slm_plan* p, int mode, const ColParams& cp, int cls) {
 int unblock_expected(slm_plan* p, const float* e_blk) {
     const dim3 grid(p->W / 64, p->H / 64, p->B);
     switch (layout_y_log2(p->lid)) {
-        case 1: return launch(p, SLM_KERNEL_OTHER, unblock_tile_kernel<1>, grid, dim3(256), e_blk, p->e_out, p->H, p->W);
-        case 2: return launch(p, SLM_KERNEL_OTHER, unblock_tile_kernel<2>, grid, dim3(256), e_blk, p->e_out, p->H, p->W);
-        case 3: return launch(p, SLM_KERNEL_OTHER, unblock_tile_kernel<3>, grid, dim3(256), e_blk, p->e_out, p->H, p->W);
-        case 4: return launch(p, SLM_KERNEL_OTHER, unblock_tile_kernel<4>, grid, dim3(256), e_blk, p->e_out, p->H, p->W);
+        case 1: return launch(p, SLM_KERNEL_OTHER, tile_relayout_kernel<float, 1, false>, grid, dim3(256), e_blk, p->e_out, p->H, p->W);
+        case 2: return launch(p, SLM_KERNEL_OTHER, tile_relayout_kernel<float, 2, false>, grid, dim3(256), e_blk, p->e_out, p->H, p->W);
+        case 3: return launch(p, SLM_KERNEL_OTHER, tile_relayout_kernel<float, 3, false>, grid, dim3(256), e_blk, p->e_out, p->H, p->W);
+        case 4: return launch(p, SLM_KERNEL_OTHER, tile_relayout_kernel<float, 4, false>, grid, dim3(256), e_blk, p->e_out, p->H, p->W);
         default: return fail(SLM_ERR_UNSUPPORTED, "no unblock kernel for panel log2 %d", layout_y_log2(p->lid));
     }
 }
@@ -1159,13 +1171,13 @@ int slm_plan_set_target(slm_plan* p, const void* tgt) {
     } else {
         hipLaunchKernelGGL(target_stats_partial_kernel<float>, dim3(nblk, p->B), dim3(kTsThreads), 0, p->stream,
                            (const float*)stage, p->holo, p->ts_part);
-        if (p->dev_tt == TGT_AMP) {
-            const int grid = (int)std::min<long long>(8192, (n + 255) / 256);
+        if (p->dev_tt == TGT_AMP) {  // a_T = sqrt(T) in the blocked layout (H, W multiples of 64)
             const int xl = layout_x_log2(p->lid);
-            auto k = xl == 1 ? amp_blocked_kernel<1> : xl == 3 ? amp_blocked_kernel<3>
-                     : xl == 4 ? amp_blocked_kernel<4> : amp_blocked_kernel<2>;
-            hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, p->stream, (const float*)stage, (float*)p->tgt, n, p->H,
-                               p->W);
+            auto k = xl == 1 ? tile_relayout_kernel<float, 1, true, true>
+                     : xl == 3 ? tile_relayout_kernel<float, 3, true, true>
+                     : xl == 4 ? tile_relayout_kernel<float, 4, true, true> : tile_relayout_kernel<float, 2, true, true>;
+            hipLaunchKernelGGL(k, dim3(p->W / 64, p->H / 64, p->B), dim3(256), 0, p->stream, (const float*)stage,
+                               (float*)p->tgt, p->H, p->W);
         } else {
             RC(relayout(layout_x_log2(p->lid), (const float*)stage, (float*)p->tgt, n, p->H, p->W, true, p->stream));
         }
