@@ -278,3 +278,34 @@ def test_prime_side_falls_back_to_dft_gemm(gpu, monkeypatch):
         assert p.engine() == ("dft-gemm", "dft-gemm")
     with gpu.Plan(gpu.ALGO_GS, 1, 99, 120, gpu.TGT_F32, False, 2) as p:
         assert p.engine() == ("mixed-radix", "mixed-radix")
+
+
+@pytest.mark.gpu
+def test_fft2_c128_integration_stub(gpu):
+    """INTEGRATION.md's ctypes stub of slm_fft2_c128, as a maintainer would
+    paste it, equals numpy.fft.ifft2 in float64 (src/move_traps.py:66)."""
+    import ctypes
+
+    _lib = ctypes.CDLL(gpu.LIB_PATH)
+    _vp, _i = ctypes.c_void_p, ctypes.c_int
+    _lib.slm_init.argtypes = [_i]
+    _lib.slm_last_error.restype = ctypes.c_char_p
+    _lib.slm_fft2_c128.argtypes = [_vp, _vp, _i, _i, _i, _i]
+
+    def _p(a):
+        return None if a is None else a.ctypes.data
+
+    def ifft2_hip(x, device=0):
+        if _lib.slm_init(device) != 0:
+            raise RuntimeError(_lib.slm_last_error().decode())
+        a = np.ascontiguousarray(x, np.complex128)
+        out = np.empty_like(a)
+        h, w = a.shape[-2:]
+        if _lib.slm_fft2_c128(_p(a), _p(out), a.size // (h * w), h, w, 1) != 0:
+            raise RuntimeError(_lib.slm_last_error().decode())
+        return out / (h * w)
+
+    img = np.zeros((768, 1024))
+    img[5, 7] = 255.0
+    img[300, 900] = 17.0
+    np.testing.assert_allclose(ifft2_hip(img), np.fft.ifft2(img), rtol=0, atol=1e-15 * 255)
