@@ -230,4 +230,6 @@ def test_gs_bright_incoming_single_trap_statistics_finite(gpu):
     assert np.isfinite(stats[0, :loops]).all() and np.isfinite(ph).all() and np.isfinite(e).all()
     _, _, ref_err = orc.gerchberg_saxton_faithful(t, loops, incoming_intensity=intensity, initial_phase=phi0)
     print(f"[overflow] single trap, a_in 1e6: errors {err} vs float64 {np.asarray(ref_err)}")
-    np.testing.assert_allclose(err, ref_err, rtol=1e-4)
+    # the run converges at once: later errors are the statistics' rounding floor
+    # (float32 partial sums: ~1e-7 of sum T^2 / S against float64's ~1e-15)
+    np.testing.assert_allclose(err, ref_err, rtol=1e-4, atol=1e-6 * float(np.max(ref_err)))
