@@ -47,6 +47,7 @@ namespace slm {
 struct GenericEngine {
     // mixed-radix back end: line plans (twiddles, digit reversal) of both sides
     bool mr = false;
+    bool big = false;        // a radix above mr::kMaxSmallRadix in either plan
     mr::LinePlan pw, ph;     // row (length W) and column (length H) transforms
     int rpw = 1;             // rows per row tile
     int cw_log2 = 0;         // columns per column tile = 2^cw_log2
@@ -365,19 +366,67 @@ bool mr_shape_ok(int H, int W) {
     return !mr_forced_gemm() && mr_radices(H, r) && mr_radices(W, r);
 }
 
-// columns per column tile: the widest (<= 16) whose LDS stays within a tile
-int mr_cw_log2(int H, int W) {
-    int c = 0;
-    while (c < 4 && ((long long)H << (c + 1)) <= mr::kTileElems && (1 << (c + 1)) <= W) ++c;
-    return c;
+bool mr_big(int H, int W) {
+    std::vector<int> rh, rw;
+    if (!mr_radices(H, rh) || !mr_radices(W, rw)) return false;
+    for (const auto* v : {&rh, &rw})
+        for (int r : *v)
+            if (r > mr::kMaxSmallRadix) return true;
+    return false;
 }
 
-// rows per row tile: as many as a tile holds, halved while the launch would
-// leave the chip short of workgroups and a tile still holds >= 2048 elements
-int mr_rpw(int B, int H, int W) {
-    int r = std::max(1, std::min(H, mr::kTileElems / W));
-    while (r > 1 && (long long)B * ((H + r - 1) / r) < 512 && (long long)(r / 2) * W >= 2048) r /= 2;
-    return r;
+// Tiles of the two launches. A launch of `wgs` workgroups of `e` elements on
+// `cus` CUs that hold `occ` of them at once takes about rounds x (workgroups
+// per CU in a round) x e: so the rows per row tile / columns per column tile
+// minimise ceil(wgs / (cus occ)) * min(occ, ceil(wgs / cus)) * e (a grid one
+// workgroup too large for a round doubles the launch: 1080 rows in 540
+// two-row tiles on 512 slots did, 62.6 against ~35 us). Ties go to the wider
+// tile (longer contiguous HBM segments). $SLM_MR_RPW / $SLM_MR_CW override.
+struct MrTiling {
+    int rpw = 1, cw_log2 = 0;
+};
+MrTiling mr_tiling(int B, int H, int W) {
+    MrTiling t;
+    const bool big = mr_big(H, W);
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+        cus = 256;
+    auto cost = [&](long long wgs, int occ, long long e) {
+        const long long slots = (long long)cus * occ;
+        const long long rounds = (wgs + slots - 1) / slots;
+        const long long per = std::min<long long>(occ, (wgs + cus - 1) / cus);
+        return rounds * per * e;
+    };
+    long long best = -1;
+    for (int r = 1; r == 1 || (long long)r * W <= mr::kTileElems; r *= 2) {
+        if (r > 1 && r > H) break;
+        const int occ = mr::mr_row_occupancy(mr::RO_GS, big, (size_t)r * W * sizeof(double2));
+        if (occ < 1) continue;
+        const long long c = cost((long long)B * ((H + r - 1) / r), occ, (long long)r * W);
+        if (best < 0 || c <= best) {
+            best = c;
+            t.rpw = r;
+        }
+    }
+    best = -1;
+    for (int c = 0; c <= 4; ++c) {
+        if (c > 0 && (((long long)H << c) > mr::kTileElems || (1 << c) > 2 * W)) break;
+        const int occ = mr::mr_col_occupancy(mr::CO_GS, big, ((size_t)H << c) * sizeof(double2));
+        if (occ < 1) continue;
+        const long long v = cost((long long)B * ((W + (1 << c) - 1) >> c), occ, (long long)H << c);
+        if (best < 0 || v <= best) {
+            best = v;
+            t.cw_log2 = c;
+        }
+    }
+    if (const char* e = std::getenv("SLM_MR_RPW")) t.rpw = std::max(1, std::min(H, std::atoi(e)));
+    if (const char* e = std::getenv("SLM_MR_CW")) {
+        int c = 0;
+        while (c < 4 && (2 << c) <= std::atoi(e)) ++c;
+        t.cw_log2 = c;
+    }
+    return t;
 }
 
 // twiddles exp(-2 pi i t / n) and the DIF output order's natural indices
@@ -454,7 +503,8 @@ int mr_row(GenericEngine* g, const GenericView& v, int op, mr::RowArgs a, int cl
     const int grid = v.B * ((v.H + g->rpw - 1) / g->rpw);
     const size_t lds = (size_t)g->rpw * v.W * sizeof(double2);
     Mark mk(v, cls);
-    if (mr::mr_row_launch(op, a, grid, lds, v.stream)) return slm_set_error(SLM_ERR_HIP, "mixed-radix row launch failed");
+    if (mr::mr_row_launch(op, g->big, a, grid, lds, v.stream))
+        return slm_set_error(SLM_ERR_HIP, "mixed-radix row launch failed");
     return 0;
 }
 
@@ -477,7 +527,8 @@ int mr_col(GenericEngine* g, const GenericView& v, int op, mr::ColArgs a, int cl
     const int grid = v.B * g->nwg_col;
     const size_t lds = ((size_t)v.H << g->cw_log2) * sizeof(double2);
     Mark mk(v, cls);
-    if (mr::mr_col_launch(op, a, grid, lds, v.stream)) return slm_set_error(SLM_ERR_HIP, "mixed-radix column launch failed");
+    if (mr::mr_col_launch(op, g->big, a, grid, lds, v.stream))
+        return slm_set_error(SLM_ERR_HIP, "mixed-radix column launch failed");
     return 0;
 }
 
@@ -570,8 +621,11 @@ int mr_enqueue(GenericEngine* g, const GenericView& v, int loops, double tol, in
 
 }  // namespace
 
-int generic_nwg(int H, int W, long long holo) {
-    if (mr_shape_ok(H, W)) return (W + (1 << mr_cw_log2(H, W)) - 1) >> mr_cw_log2(H, W);
+int generic_nwg(int B, int H, int W, long long holo) {
+    if (mr_shape_ok(H, W)) {
+        const MrTiling t = mr_tiling(B, H, W);
+        return (W + (1 << t.cw_log2) - 1) >> t.cw_log2;
+    }
     return (int)std::max<long long>(1, std::min<long long>(1024, holo / (kGT * 8)));
 }
 
@@ -601,9 +655,11 @@ int generic_create(const GenericView& v, GenericEngine** out) {
     };
     if (mr_shape_ok(v.H, v.W)) {  // mixed radix: two state buffers (+ the GD field), line plans
         g->mr = true;
-        g->cw_log2 = mr_cw_log2(v.H, v.W);
+        g->big = mr_big(v.H, v.W);
+        const MrTiling t = mr_tiling(v.B, v.H, v.W);
+        g->cw_log2 = t.cw_log2;
         g->nwg_col = (v.W + (1 << g->cw_log2) - 1) >> g->cw_log2;
-        g->rpw = mr_rpw(v.B, v.H, v.W);
+        g->rpw = t.rpw;
         if (g->nwg_col != v.nwg) return fail_free(slm_set_error(SLM_ERR_STATE, "mixed radix: partial-slab mismatch"));
         if (!alloc(&g->a, n) || !alloc(&g->b, n) || (v.algo == SLM_ALGO_GD && !alloc(&g->x, n)))
             return fail_free(slm_set_error(SLM_ERR_HIP, "mixed radix: device allocation failed"));

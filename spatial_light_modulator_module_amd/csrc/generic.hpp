@@ -38,7 +38,7 @@ struct GenericView {
 
 // statistics blocks per hologram (the partials' nwg): column tiles of the
 // mixed-radix back end, element chunks of the DFT-GEMM one
-int generic_nwg(int H, int W, long long holo);
+int generic_nwg(int B, int H, int W, long long holo);
 // true for the DFT-GEMM back end (rocBLAS calls: runs are not graph-captured)
 bool generic_uses_blas(const GenericEngine* g);
 int generic_create(const GenericView& v, GenericEngine** out);

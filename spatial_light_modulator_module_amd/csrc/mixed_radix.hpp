@@ -43,12 +43,17 @@
 namespace slm {
 namespace mr {
 
-constexpr int kThreads = 512;  // threads per workgroup of every mixed-radix kernel
+constexpr int kThreads = 256;  // threads per workgroup of every mixed-radix kernel
 constexpr int kMaxPass = 16;
 constexpr int kMaxRadix = 13;
 // LDS of one tile: at most this many complex128 elements (72 KiB: two
 // workgroups per CU); a single line may take up to kMaxLine (one per CU)
 constexpr int kTileElems = 4608;
+// radices above 8 (7, 11, 13) cost registers in every pass of a kernel that
+// can run them (generic odd DFTs): plans without them take kernels built for
+// radix <= 8 only (60-85 VGPRs, five 4-wave workgroups per CU) and plans with
+// them the full set (<= 128 VGPRs, four)
+constexpr int kMaxSmallRadix = 8;
 constexpr int kMaxLine = 8192;
 
 // one line length's plan: radices in DIF stage order, the twiddle table
@@ -213,38 +218,44 @@ __device__ __forceinline__ void pass(double2* lds, const Lines& g, int n, int L,
     __syncthreads();
 }
 
-template <bool INV, bool LINEFAST, bool DIT>
+template <bool INV, bool LINEFAST, bool DIT, bool BIG>
 __device__ __forceinline__ void pass_r(int R, double2* lds, const Lines& g, int n, int L, const double2* tw) {
     switch (R) {
         case 2: pass<2, INV, LINEFAST, DIT>(lds, g, n, L, tw); break;
         case 3: pass<3, INV, LINEFAST, DIT>(lds, g, n, L, tw); break;
         case 4: pass<4, INV, LINEFAST, DIT>(lds, g, n, L, tw); break;
         case 5: pass<5, INV, LINEFAST, DIT>(lds, g, n, L, tw); break;
-        case 7: pass<7, INV, LINEFAST, DIT>(lds, g, n, L, tw); break;
         case 8: pass<8, INV, LINEFAST, DIT>(lds, g, n, L, tw); break;
-        case 11: pass<11, INV, LINEFAST, DIT>(lds, g, n, L, tw); break;
-        default: pass<13, INV, LINEFAST, DIT>(lds, g, n, L, tw); break;
+        default:
+            if constexpr (BIG) {
+                switch (R) {
+                    case 7: pass<7, INV, LINEFAST, DIT>(lds, g, n, L, tw); break;
+                    case 11: pass<11, INV, LINEFAST, DIT>(lds, g, n, L, tw); break;
+                    default: pass<13, INV, LINEFAST, DIT>(lds, g, n, L, tw); break;
+                }
+            }
+            break;
     }
 }
 
 // natural order in -> digit-reversed (rev) order out, every line of the tile
-template <bool INV, bool LINEFAST>
+template <bool INV, bool LINEFAST, bool BIG>
 __device__ __forceinline__ void fft_dif(double2* lds, const Lines& g, const LinePlan& pl) {
     int L = pl.n;
     for (int s = 0; s < pl.np; ++s) {
         const int R = pl.radix[s];
-        pass_r<INV, LINEFAST, false>(R, lds, g, pl.n, L, pl.tw);
+        pass_r<INV, LINEFAST, false, BIG>(R, lds, g, pl.n, L, pl.tw);
         L /= R;
     }
 }
 // digit-reversed order in -> natural order out
-template <bool INV, bool LINEFAST>
+template <bool INV, bool LINEFAST, bool BIG>
 __device__ __forceinline__ void fft_dit(double2* lds, const Lines& g, const LinePlan& pl) {
     int L = 1;
     for (int s = pl.np - 1; s >= 0; --s) {
         const int R = pl.radix[s];
         L *= R;
-        pass_r<INV, LINEFAST, true>(R, lds, g, pl.n, L, pl.tw);
+        pass_r<INV, LINEFAST, true, BIG>(R, lds, g, pl.n, L, pl.tw);
     }
 }
 
@@ -310,9 +321,13 @@ struct ColArgs {
     LinePlan pl;                       // length H
 };
 
-// host launchers (mr_inst.hip; lds = tile elements x 16 B; 0 or -1 on a launch error)
-int mr_row_launch(int op, const RowArgs& a, int grid, size_t lds, hipStream_t st);
-int mr_col_launch(int op, const ColArgs& a, int grid, size_t lds, hipStream_t st);
+// host launchers (mr_inst.hip; big: a plan radix above kMaxSmallRadix; lds =
+// tile elements x 16 B; 0 or -1 on a launch error)
+int mr_row_launch(int op, bool big, const RowArgs& a, int grid, size_t lds, hipStream_t st);
+int mr_col_launch(int op, bool big, const ColArgs& a, int grid, size_t lds, hipStream_t st);
+// workgroups of one kernel a CU holds at once (occupancy query; 0 on error)
+int mr_row_occupancy(int op, bool big, size_t lds);
+int mr_col_occupancy(int op, bool big, size_t lds);
 // small-DFT roots (host table [kMaxRadix + 1][kMaxRadix]) into the current device's copy
 int mr_set_roots(const double2* roots, hipStream_t st);
 

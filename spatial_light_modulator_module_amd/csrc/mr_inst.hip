@@ -19,9 +19,11 @@ namespace slm {
 namespace mr {
 namespace {
 
-// waves per SIMD the register budget must allow: 4 = two 512-thread
-// workgroups per CU (<= 128 VGPRs), which their LDS (<= 72 KiB each) allows
-constexpr int kWavesPerSimd = 4;
+// waves per SIMD the register budget must allow: 5 (<= 102 VGPRs: five
+// 4-wave workgroups per CU) for kernels with radices up to 8, 4 (<= 128) with
+// the odd radices 7, 11, 13
+template <bool BIG>
+constexpr int kWavesPerSimd = BIG ? 4 : 5;
 
 __device__ __forceinline__ double amp_of(const void* tgt, int tt, long long i) {
     if (tt == TGT_U8) return (double)TgtLoad<TGT_U8>::amp(TgtLoad<TGT_U8>::load(tgt, i));
@@ -44,12 +46,13 @@ __device__ __forceinline__ double2 u_of(double2 x, double a) {
 }
 __device__ __forceinline__ double2 round_c64(double2 z) { return make_double2((double)(float)z.x, (double)(float)z.y); }
 
-template <int OP>
-__global__ void __launch_bounds__(kThreads, kWavesPerSimd) mr_row_kernel(RowArgs a) {
+template <int OP, bool BIG>
+__global__ void __launch_bounds__(kThreads, kWavesPerSimd<BIG>) mr_row_kernel(RowArgs a) {
     extern __shared__ double2 lds[];
     const int tiles = (a.H + a.rpw - 1) / a.rpw;
-    const int b = blockIdx.x / tiles;
-    const int row0 = (blockIdx.x - b * tiles) * a.rpw;
+    const int id = xcd_remap(blockIdx.x, gridDim.x);  // neighbouring tiles on one XCD
+    const int b = id / tiles;
+    const int row0 = (id - b * tiles) * a.rpw;
     const int rows = min(a.rpw, a.H - row0);
     const int W = a.W;
     const int ne = rows * W;
@@ -92,9 +95,9 @@ __global__ void __launch_bounds__(kThreads, kWavesPerSimd) mr_row_kernel(RowArgs
     __syncthreads();
     const Lines g{rows, W, 1};
     if constexpr (GATHER) {
-        fft_dit<OP == RO_INV, false>(lds, g, a.pl);
+        fft_dit<OP == RO_INV, false, BIG>(lds, g, a.pl);
     } else {
-        fft_dif<true, false>(lds, g, a.pl);  // inverse: A (GS), the gradient (GD), A0 (setup)
+        fft_dif<true, false, BIG>(lds, g, a.pl);  // inverse: A (GS), the gradient (GD), A0 (setup)
         // projection on the digit-reversed order, between the inverse and the forward transform
         const bool phase_only = OP == RO_GS && (a.last || (a.checked && a.stop[b] == a.iter));
         const double l = OP == RO_GD ? (double)a.lr[a.iter] : 0.0;
@@ -136,16 +139,17 @@ __global__ void __launch_bounds__(kThreads, kWavesPerSimd) mr_row_kernel(RowArgs
         // (uniform per workgroup) the run's last GD update needs no next forward transform
         if (phase_only || (OP == RO_GD && a.last)) return;
         __syncthreads();
-        fft_dit<false, false>(lds, g, a.pl);
+        fft_dit<false, false, BIG>(lds, g, a.pl);
     }
     for (int e = threadIdx.x; e < ne; e += kThreads) a.out[off + e] = lds[e];
 }
 
-template <int OP>
-__global__ void __launch_bounds__(kThreads, kWavesPerSimd) mr_col_kernel(ColArgs a) {
+template <int OP, bool BIG>
+__global__ void __launch_bounds__(kThreads, kWavesPerSimd<BIG>) mr_col_kernel(ColArgs a) {
     extern __shared__ double2 lds[];
-    const int b = blockIdx.x / a.nwg;
-    const int tile = blockIdx.x - b * a.nwg;
+    const int id = xcd_remap(blockIdx.x, gridDim.x);  // neighbouring tiles (partial lines) on one XCD
+    const int b = id / a.nwg;
+    const int tile = id - b * a.nwg;
     const int cw = 1 << a.cw_log2;
     const int c0 = tile * cw;
     const int ne = a.H * cw;
@@ -177,9 +181,9 @@ __global__ void __launch_bounds__(kThreads, kWavesPerSimd) mr_col_kernel(ColArgs
     __syncthreads();
     const Lines g{cw, 1, cw};
     if constexpr (GATHER) {
-        fft_dit<OP != CO_FWD, true>(lds, g, a.pl);
+        fft_dit<OP != CO_FWD, true, BIG>(lds, g, a.pl);
     } else {
-        fft_dif<false, true>(lds, g, a.pl);  // C (GS), F (GD)
+        fft_dif<false, true, BIG>(lds, g, a.pl);  // C (GS), F (GD)
         double mx = 0.0, s2 = 0.0, st = 0.0, s = 0.0;
         if constexpr (OP == CO_GD_GRAD) s = a.norm[b] / a.stats[((long long)b * a.max_loops + a.iter) * 4];
         for (int e = threadIdx.x; e < ne; e += kThreads) {
@@ -216,7 +220,7 @@ __global__ void __launch_bounds__(kThreads, kWavesPerSimd) mr_col_kernel(ColArgs
         }
         if constexpr (OP == CO_GD_STATS) return;
         __syncthreads();
-        fft_dit<true, true>(lds, g, a.pl);
+        fft_dit<true, true, BIG>(lds, g, a.pl);
     }
     for (int e = threadIdx.x; e < ne; e += kThreads) {
         long long i;
@@ -231,46 +235,70 @@ bool raise_lds(F fn) {
            hipSuccess;
 }
 
-template <int OP>
+template <int OP, bool BIG>
 int row_one(const RowArgs& a, int grid, size_t lds, hipStream_t st) {
-    static const bool ok = raise_lds(mr_row_kernel<OP>);
+    static const bool ok = raise_lds(mr_row_kernel<OP, BIG>);
     if (!ok) return -1;
-    hipLaunchKernelGGL(mr_row_kernel<OP>, dim3(grid), dim3(kThreads), lds, st, a);
+    hipLaunchKernelGGL((mr_row_kernel<OP, BIG>), dim3(grid), dim3(kThreads), lds, st, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
-template <int OP>
+template <int OP, bool BIG>
 int col_one(const ColArgs& a, int grid, size_t lds, hipStream_t st) {
-    static const bool ok = raise_lds(mr_col_kernel<OP>);
+    static const bool ok = raise_lds(mr_col_kernel<OP, BIG>);
     if (!ok) return -1;
-    hipLaunchKernelGGL(mr_col_kernel<OP>, dim3(grid), dim3(kThreads), lds, st, a);
+    hipLaunchKernelGGL((mr_col_kernel<OP, BIG>), dim3(grid), dim3(kThreads), lds, st, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+template <class F>
+int occupancy_of(F fn, size_t lds) {
+    if (!raise_lds(fn)) return 0;
+    int n = 0;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)fn, kThreads, lds) == hipSuccess ? n : 0;
+}
+
+template <bool BIG>
+int row_launch(int op, const RowArgs& a, int grid, size_t lds, hipStream_t st) {
+    switch (op) {
+        case RO_FWD: return row_one<RO_FWD, BIG>(a, grid, lds, st);
+        case RO_INV: return row_one<RO_INV, BIG>(a, grid, lds, st);
+        case RO_COLD: return row_one<RO_COLD, BIG>(a, grid, lds, st);
+        case RO_WARM: return row_one<RO_WARM, BIG>(a, grid, lds, st);
+        case RO_GS: return row_one<RO_GS, BIG>(a, grid, lds, st);
+        case RO_GD_FOURIER: return row_one<RO_GD_FOURIER, BIG>(a, grid, lds, st);
+        case RO_GD_INIT: return row_one<RO_GD_INIT, BIG>(a, grid, lds, st);
+        case RO_GD: return row_one<RO_GD, BIG>(a, grid, lds, st);
+        default: return -1;
+    }
+}
+template <bool BIG>
+int col_launch(int op, const ColArgs& a, int grid, size_t lds, hipStream_t st) {
+    switch (op) {
+        case CO_FWD: return col_one<CO_FWD, BIG>(a, grid, lds, st);
+        case CO_INV: return col_one<CO_INV, BIG>(a, grid, lds, st);
+        case CO_AMP_INV: return col_one<CO_AMP_INV, BIG>(a, grid, lds, st);
+        case CO_GS: return col_one<CO_GS, BIG>(a, grid, lds, st);
+        case CO_GD_STATS: return col_one<CO_GD_STATS, BIG>(a, grid, lds, st);
+        case CO_GD_GRAD: return col_one<CO_GD_GRAD, BIG>(a, grid, lds, st);
+        default: return -1;
+    }
 }
 
 }  // namespace
 
-int mr_row_launch(int op, const RowArgs& a, int grid, size_t lds, hipStream_t st) {
-    switch (op) {
-        case RO_FWD: return row_one<RO_FWD>(a, grid, lds, st);
-        case RO_INV: return row_one<RO_INV>(a, grid, lds, st);
-        case RO_COLD: return row_one<RO_COLD>(a, grid, lds, st);
-        case RO_WARM: return row_one<RO_WARM>(a, grid, lds, st);
-        case RO_GS: return row_one<RO_GS>(a, grid, lds, st);
-        case RO_GD_FOURIER: return row_one<RO_GD_FOURIER>(a, grid, lds, st);
-        case RO_GD_INIT: return row_one<RO_GD_INIT>(a, grid, lds, st);
-        case RO_GD: return row_one<RO_GD>(a, grid, lds, st);
-        default: return -1;
-    }
+int mr_row_launch(int op, bool big, const RowArgs& a, int grid, size_t lds, hipStream_t st) {
+    return big ? row_launch<true>(op, a, grid, lds, st) : row_launch<false>(op, a, grid, lds, st);
 }
-int mr_col_launch(int op, const ColArgs& a, int grid, size_t lds, hipStream_t st) {
-    switch (op) {
-        case CO_FWD: return col_one<CO_FWD>(a, grid, lds, st);
-        case CO_INV: return col_one<CO_INV>(a, grid, lds, st);
-        case CO_AMP_INV: return col_one<CO_AMP_INV>(a, grid, lds, st);
-        case CO_GS: return col_one<CO_GS>(a, grid, lds, st);
-        case CO_GD_STATS: return col_one<CO_GD_STATS>(a, grid, lds, st);
-        case CO_GD_GRAD: return col_one<CO_GD_GRAD>(a, grid, lds, st);
-        default: return -1;
-    }
+int mr_col_launch(int op, bool big, const ColArgs& a, int grid, size_t lds, hipStream_t st) {
+    return big ? col_launch<true>(op, a, grid, lds, st) : col_launch<false>(op, a, grid, lds, st);
+}
+// the iteration kernels' occupancy (the setup kernels share their shape)
+int mr_row_occupancy(int op, bool big, size_t lds) {
+    (void)op;
+    return big ? occupancy_of(mr_row_kernel<RO_GS, true>, lds) : occupancy_of(mr_row_kernel<RO_GS, false>, lds);
+}
+int mr_col_occupancy(int op, bool big, size_t lds) {
+    (void)op;
+    return big ? occupancy_of(mr_col_kernel<CO_GS, true>, lds) : occupancy_of(mr_col_kernel<CO_GS, false>, lds);
 }
 int mr_set_roots(const double2* roots, hipStream_t st) {
     if (hipMemcpyToSymbolAsync(HIP_SYMBOL(kRoots), roots, sizeof(kRoots), 0, hipMemcpyHostToDevice, st) != hipSuccess)

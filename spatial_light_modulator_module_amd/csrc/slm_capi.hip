@@ -1045,7 +1045,7 @@ int plan_create_on(int device, int algo, int batch, int height, int width, int t
         p->prec = PREC_F64;
         p->lid = LAYOUT_DEFAULT;
         p->cw = 0;
-        p->nwg = max_nwg = generic_nwg(height, width, p->holo);
+        p->nwg = max_nwg = generic_nwg(batch, height, width, p->holo);
         p->rpw = min_rpw = 1;
     } else {
         const int want = p->prec;
@@ -1660,7 +1660,7 @@ int slm_fft2_c128(const double* in, double* out, int batch, int height, int widt
     q.W = width;
     q.holo = (long long)height * width;
     q.max_loops = 1;
-    q.nwg = generic_nwg(height, width, q.holo);
+    q.nwg = generic_nwg(batch, height, width, q.holo);
     q.device = g_device;
     HIP_TRY(hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking));
     const size_t bytes = (size_t)batch * q.holo * sizeof(double2);
