@@ -290,7 +290,14 @@ def secondary(n, batch, iters, algo=_lib.ALGO_GS, precision=None, reps=3, width=
     for k, row in rows.items():
         row["traffic_bytes_per_launch"] = None if traffic is None else traffic.get(k)
     per_px = 76 if algo == _lib.ALGO_GD else 68
+    # the north-star fraction on bytes moved: the committed rocprofv3 PMC traffic
+    # (FETCH_SIZE x 2 + WRITE_SIZE per launch, profiles/pmc_traffic.json) of one
+    # column and one row launch -- a GS iteration -- over the measured iteration time
+    pmc_frac = None
+    if traffic and algo == _lib.ALGO_GS and traffic.get("col_main") and traffic.get("row_main"):
+        pmc_frac = round((traffic["col_main"] + traffic["row_main"]) / iter_s / 1e9 / HBM_PEAK_GBS, 4)
     return {"algo": name, "shape": [batch, n, w], "iters": iters, "engine": list(plan_engine),
+            "iter_frac_of_hbm_peak_pmc": pmc_frac,
             "holograms_per_s": batch / wall, "iter_ms": iter_s * 1e3, "iter_ms_per_hologram": iter_s * 1e3 / batch,
             "iter_frac_of_hbm_peak_model": round(per_px * batch * n * w / iter_s / 1e9 / HBM_PEAK_GBS, 4),
             "iter_frac_of_hbm_peak_physical": round(phys_iter / iter_s / 1e9 / HBM_PEAK_GBS, 4),

@@ -45,6 +45,12 @@
 // Twiddles: 16 per thread (7 + 3 + 2 x 3), read once from a table of the 1024
 // roots exp(-2 pi i e / 1024) computed in double on the host (slm_capi.hip,
 // get_twiddles) and shared by both transforms (the second uses conjugates).
+//
+// Arithmetic type C: float2 (float32 butterflies) or double2 (float64
+// butterflies and twiddles, the values held in double between the passes and
+// moved by the lane swaps as two dword pairs; the one LDS exchange X2 stores
+// complex64). The plan's state in HBM is complex64 either way; callers hand in
+// complex64 slots and get complex64 back (shuffle_pair converts).
 #pragma once
 #include "fft_core.hpp"
 
@@ -59,13 +65,16 @@ __device__ __forceinline__ int shuffle_t(int tid) {
     return ((lam >> 1) & 7) | (om << 3) | (((lam >> 4) & 3) << 5);
 }
 
-struct ShuffleTw {
-    float2 p1[7];  // w_1024^(t k1), k1 = 1..7
-    float2 p2[3];  // w_128^((t & 31) k2), k2 = 1..3
-    float2 p3[6];  // w_32^(n k3), n = l4 + 2 l5 + 4 s2, [3 s2 + k3 - 1]
+template <class C>
+struct ShuffleTwT {
+    C p1[7];  // w_1024^(t k1), k1 = 1..7
+    C p2[3];  // w_128^((t & 31) k2), k2 = 1..3
+    C p3[6];  // w_32^(n k3), n = l4 + 2 l5 + 4 s2, [3 s2 + k3 - 1]
 };
+using ShuffleTw = ShuffleTwT<float2>;
 
-__device__ __forceinline__ void load_shuffle_tw(ShuffleTw& tw, int tid, const float2* __restrict__ roots) {
+template <class C>
+__device__ __forceinline__ void load_shuffle_tw(ShuffleTwT<C>& tw, int tid, const C* __restrict__ roots) {
     const int t = shuffle_t(tid);
     const int lam = tid & 63;
     static_for<7>([&](auto kc) {
@@ -103,8 +112,32 @@ __device__ __forceinline__ void swap_l5(float2& a, float2& b) {
     a = make_float2(as_f(x[0]), as_f(y[0]));
     b = make_float2(as_f(x[1]), as_f(y[1]));
 }
+// float64 values: each half of each component is one dword swap
+__device__ __forceinline__ unsigned lo_u(double x) { return (unsigned)__builtin_bit_cast(unsigned long long, x); }
+__device__ __forceinline__ unsigned hi_u(double x) { return (unsigned)(__builtin_bit_cast(unsigned long long, x) >> 32); }
+__device__ __forceinline__ double as_d(unsigned lo, unsigned hi) {
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+template <bool HALVES32>
+__device__ __forceinline__ void swap_d(double& a, double& b) {
+    const auto l = HALVES32 ? __builtin_amdgcn_permlane32_swap(lo_u(a), lo_u(b), false, false)
+                            : __builtin_amdgcn_permlane16_swap(lo_u(a), lo_u(b), false, false);
+    const auto h = HALVES32 ? __builtin_amdgcn_permlane32_swap(hi_u(a), hi_u(b), false, false)
+                            : __builtin_amdgcn_permlane16_swap(hi_u(a), hi_u(b), false, false);
+    a = as_d(l[0], h[0]);
+    b = as_d(l[1], h[1]);
+}
+__device__ __forceinline__ void swap_l4(double2& a, double2& b) {
+    swap_d<false>(a.x, b.x);
+    swap_d<false>(a.y, b.y);
+}
+__device__ __forceinline__ void swap_l5(double2& a, double2& b) {
+    swap_d<true>(a.x, b.x);
+    swap_d<true>(a.y, b.y);
+}
 // X1: s1 <-> l4, s2 <-> l5 (its own inverse)
-__device__ __forceinline__ void shuffle_x1(float2 (&v)[8]) {
+template <class C>
+__device__ __forceinline__ void shuffle_x1(C (&v)[8]) {
     swap_l4(v[0], v[2]);
     swap_l4(v[1], v[3]);
     swap_l4(v[4], v[6]);
@@ -115,7 +148,8 @@ __device__ __forceinline__ void shuffle_x1(float2 (&v)[8]) {
     swap_l5(v[3], v[7]);
 }
 // X3: s0 <-> l4, s1 <-> l5 (its own inverse)
-__device__ __forceinline__ void shuffle_x3(float2 (&v)[8]) {
+template <class C>
+__device__ __forceinline__ void shuffle_x3(C (&v)[8]) {
     swap_l4(v[0], v[1]);
     swap_l4(v[2], v[3]);
     swap_l4(v[4], v[5]);
@@ -147,30 +181,30 @@ __device__ __forceinline__ int shuffle_slot(int p, int line) {
     const int h = j2 | (j0 << 1) | (j1 << 2) | ((line ^ j2) << 3) | ((j2 ^ j1) << 4);
     return line * kShufN + (p ^ h);
 }
-template <bool B_TO_C>
-__device__ __forceinline__ void shuffle_x2(float2 (&v)[8], int tid, float2* buf) {
+template <bool B_TO_C, class C>
+__device__ __forceinline__ void shuffle_x2(C (&v)[8], int tid, float2* buf) {
     const int line = tid & 1;
     static_for<8>([&](auto mc) {
         constexpr int m = decltype(mc)::value;
-        buf[shuffle_slot(B_TO_C ? shuffle_pos_b(tid, m) : shuffle_pos_c(tid, m), line)] = v[m];
+        buf[shuffle_slot(B_TO_C ? shuffle_pos_b(tid, m) : shuffle_pos_c(tid, m), line)] = cv<float2>(v[m]);
     });
     lds_barrier();
     static_for<8>([&](auto mc) {
         constexpr int m = decltype(mc)::value;
-        v[m] = buf[shuffle_slot(B_TO_C ? shuffle_pos_c(tid, m) : shuffle_pos_b(tid, m), line)];
+        v[m] = cv<C>(buf[shuffle_slot(B_TO_C ? shuffle_pos_c(tid, m) : shuffle_pos_b(tid, m), line)]);
     });
 }
 
 // --- passes -------------------------------------------------------------------
 // DIF: butterfly, then twiddle; DIT (adjoint): twiddle, then butterfly.
-template <bool INV>
-__device__ __forceinline__ float2 tw_mul(float2 a, float2 w) {
+template <bool INV, class C>
+__device__ __forceinline__ C tw_mul(C a, C w) {
     return INV ? cmulc(a, w) : cmul(a, w);
 }
 // radix-4 butterflies over slots {base + stride d}, twiddles w[0..2] after (DIF) or before (DIT)
-template <bool INV, bool DIF, int BASE, int STRIDE>
-__device__ __forceinline__ void shuffle_r4(float2 (&v)[8], const float2* w) {
-    float2 u[4];
+template <bool INV, bool DIF, int BASE, int STRIDE, class C>
+__device__ __forceinline__ void shuffle_r4(C (&v)[8], const C* w) {
+    C u[4];
     static_for<4>([&](auto dc) {
         constexpr int d = decltype(dc)::value;
         u[d] = v[BASE + STRIDE * d];
@@ -181,7 +215,7 @@ __device__ __forceinline__ void shuffle_r4(float2 (&v)[8], const float2* w) {
             u[r] = tw_mul<INV>(u[r], w[r - 1]);
         });
     }
-    Dft<4, INV, float2>::run(u);
+    Dft<4, INV, C>::run(u);
     if constexpr (DIF) {
         static_for<3>([&](auto rc) {
             constexpr int r = decltype(rc)::value + 1;
@@ -193,15 +227,15 @@ __device__ __forceinline__ void shuffle_r4(float2 (&v)[8], const float2* w) {
         v[BASE + STRIDE * d] = u[d];
     });
 }
-template <bool INV, bool DIF>
-__device__ __forceinline__ void shuffle_p1(float2 (&v)[8], const ShuffleTw& tw) {
+template <bool INV, bool DIF, class C>
+__device__ __forceinline__ void shuffle_p1(C (&v)[8], const ShuffleTwT<C>& tw) {
     if constexpr (!DIF) {
         static_for<7>([&](auto rc) {
             constexpr int r = decltype(rc)::value + 1;
             v[r] = tw_mul<INV>(v[r], tw.p1[r - 1]);
         });
     }
-    Dft<8, INV, float2>::run(v);
+    Dft<8, INV, C>::run(v);
     if constexpr (DIF) {
         static_for<7>([&](auto rc) {
             constexpr int r = decltype(rc)::value + 1;
@@ -209,13 +243,13 @@ __device__ __forceinline__ void shuffle_p1(float2 (&v)[8], const ShuffleTw& tw) 
         });
     }
 }
-template <bool INV, bool DIF>
-__device__ __forceinline__ void shuffle_p2(float2 (&v)[8], const ShuffleTw& tw) {
+template <bool INV, bool DIF, class C>
+__device__ __forceinline__ void shuffle_p2(C (&v)[8], const ShuffleTwT<C>& tw) {
     shuffle_r4<INV, DIF, 0, 2>(v, tw.p2);  // s0 = 0: slots 0, 2, 4, 6
     shuffle_r4<INV, DIF, 1, 2>(v, tw.p2);  // s0 = 1
 }
-template <bool INV, bool DIF>
-__device__ __forceinline__ void shuffle_p3(float2 (&v)[8], const ShuffleTw& tw) {
+template <bool INV, bool DIF, class C>
+__device__ __forceinline__ void shuffle_p3(C (&v)[8], const ShuffleTwT<C>& tw) {
     shuffle_r4<INV, DIF, 0, 1>(v, tw.p3);      // s2 = 0: slots 0..3
     shuffle_r4<INV, DIF, 4, 1>(v, tw.p3 + 3);  // s2 = 1: slots 4..7
 }
@@ -223,22 +257,22 @@ __device__ __forceinline__ void shuffle_p3(float2 (&v)[8], const ShuffleTw& tw) 
 // First transform of a pair (INV, decimated in frequency): state A in, state
 // D out -- slot m of the thread then holds element (frequency) t + 128 m.
 // Every thread of the workgroup must call it (LDS barrier); lds: 2048 complex64.
-template <bool INV>
-__device__ __forceinline__ void shuffle_first_scalar(float2 (&v)[8], int tid, const ShuffleTw& tw, float2* lds) {
+template <bool INV, class C>
+__device__ __forceinline__ void shuffle_first_scalar(C (&v)[8], int tid, const ShuffleTwT<C>& tw, float2* lds) {
     shuffle_p1<INV, true>(v, tw);
     shuffle_x1(v);
     shuffle_p2<INV, true>(v, tw);
     shuffle_x2<true>(v, tid, lds);
     shuffle_p3<INV, true>(v, tw);
     shuffle_x3(v);
-    Dft<8, INV, float2>::run(v);
+    Dft<8, INV, C>::run(v);
 }
 // Second transform (INV, decimated in time, the adjoint schedule): state D in,
 // state A out. lds: 2048 complex64, not the buffer of the first transform
 // (one barrier per exchange then suffices).
-template <bool INV>
-__device__ __forceinline__ void shuffle_second_scalar(float2 (&v)[8], int tid, const ShuffleTw& tw, float2* lds) {
-    Dft<8, INV, float2>::run(v);
+template <bool INV, class C>
+__device__ __forceinline__ void shuffle_second_scalar(C (&v)[8], int tid, const ShuffleTwT<C>& tw, float2* lds) {
+    Dft<8, INV, C>::run(v);
     shuffle_x3(v);
     shuffle_p3<INV, false>(v, tw);
     shuffle_x2<false>(v, tid, lds);
@@ -247,25 +281,46 @@ __device__ __forceinline__ void shuffle_second_scalar(float2 (&v)[8], int tid, c
     shuffle_p1<INV, false>(v, tw);
 }
 
-// Transform (INV1), epi(0, m, z) on every output (slot m = element t + 128 m),
-// transform (INV2); v in state A in and out. lds: 2 x 2048 complex64.
-template <bool INV>
-__device__ __forceinline__ void shuffle_first(float2 (&v)[8], int tid, const ShuffleTw& tw, float2* lds) {
-    shuffle_first_scalar<INV>(v, tid, tw, lds);
+// First / second transform on complex64 slots v in the arithmetic type C of
+// the twiddles (float32: in place; float64: widened for the transform and
+// rounded back to complex64 after it).
+template <bool INV, class C>
+__device__ __forceinline__ void shuffle_first(float2 (&v)[8], int tid, const ShuffleTwT<C>& tw, float2* lds) {
+    if constexpr (std::is_same_v<C, float2>) {
+        shuffle_first_scalar<INV>(v, tid, tw, lds);
+    } else {
+        C u[8];
+        static_for<8>([&](auto mc) { u[decltype(mc)::value] = cv<C>(v[decltype(mc)::value]); });
+        shuffle_first_scalar<INV>(u, tid, tw, lds);
+        static_for<8>([&](auto mc) { v[decltype(mc)::value] = cv<float2>(u[decltype(mc)::value]); });
+    }
 }
-template <bool INV>
-__device__ __forceinline__ void shuffle_second(float2 (&v)[8], int tid, const ShuffleTw& tw, float2* lds) {
-    shuffle_second_scalar<INV>(v, tid, tw, lds);
+template <bool INV, class C>
+__device__ __forceinline__ void shuffle_second(float2 (&v)[8], int tid, const ShuffleTwT<C>& tw, float2* lds) {
+    if constexpr (std::is_same_v<C, float2>) {
+        shuffle_second_scalar<INV>(v, tid, tw, lds);
+    } else {
+        C u[8];
+        static_for<8>([&](auto mc) { u[decltype(mc)::value] = cv<C>(v[decltype(mc)::value]); });
+        shuffle_second_scalar<INV>(u, tid, tw, lds);
+        static_for<8>([&](auto mc) { v[decltype(mc)::value] = cv<float2>(u[decltype(mc)::value]); });
+    }
 }
 
-template <bool INV1, bool INV2, class Epi>
-__device__ __forceinline__ void shuffle_pair(float2 (&v)[8], int tid, const ShuffleTw& tw, float2* lds, Epi&& epi) {
-    shuffle_first<INV1>(v, tid, tw, lds);
+// Transform (INV1), epi(0, m, z) on every output (slot m = element t + 128 m,
+// z in the arithmetic type C), transform (INV2); v in state A in and out
+// (complex64). lds: 2 x 2048 complex64.
+template <bool INV1, bool INV2, class C, class Epi>
+__device__ __forceinline__ void shuffle_pair(float2 (&v)[8], int tid, const ShuffleTwT<C>& tw, float2* lds, Epi&& epi) {
+    C u[8];
+    static_for<8>([&](auto mc) { u[decltype(mc)::value] = cv<C>(v[decltype(mc)::value]); });
+    shuffle_first_scalar<INV1>(u, tid, tw, lds);
     static_for<8>([&](auto mc) {
         constexpr int m = decltype(mc)::value;
-        epi(0, m, v[m]);
+        epi(0, m, u[m]);
     });
-    shuffle_second<INV2>(v, tid, tw, lds + 2 * kShufN);
+    shuffle_second_scalar<INV2>(u, tid, tw, lds + 2 * kShufN);
+    static_for<8>([&](auto mc) { v[decltype(mc)::value] = cv<float2>(u[decltype(mc)::value]); });
 }
 
 }  // namespace slm

@@ -47,7 +47,7 @@ namespace slm {
 struct GenericEngine {
     // mixed-radix back end: line plans (twiddles, digit reversal) of both sides
     bool mr = false;
-    bool big = false;        // a radix above mr::kMaxSmallRadix in either plan
+    bool big = false;        // a radix outside mr::small_radix in either plan (7, 11, 13)
     mr::LinePlan pw, ph;     // row (length W) and column (length H) transforms
     int rpw = 1;             // rows per row tile
     int cw_log2 = 0;         // columns per column tile = 2^cw_log2
@@ -371,7 +371,7 @@ bool mr_big(int H, int W) {
     if (!mr_radices(H, rh) || !mr_radices(W, rw)) return false;
     for (const auto* v : {&rh, &rw})
         for (int r : *v)
-            if (r > mr::kMaxSmallRadix) return true;
+            if (!mr::small_radix(r)) return true;
     return false;
 }
 

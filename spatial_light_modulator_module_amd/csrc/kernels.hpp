@@ -640,8 +640,10 @@ constexpr bool kLdsDouble = K == 11;
 // 4096-point shuffle pair for the float32 rows measured slower, 862 against
 // 788 us per 8 x 4096^2 row pass, and failed the float32 +100 gate at 1.02e-5:
 // profiles/r04/ab_shuf4096_s1.txt.)
+// Float64 butterflies run the pair too (double values between its passes, the
+// LDS exchange in complex64), for the GS iteration kernels.
 template <int K, int P>
-constexpr bool kShuffle = P == PREC_F32 && PlanOf<K>::N == kShufN && PlanOf<K>::E == 8;
+constexpr bool kShuffle = PlanOf<K>::N == kShufN && PlanOf<K>::E == 8;
 
 template <int K, int MODE, int P, int LID>
 __global__ void __launch_bounds__((RowCfg<K, P>::THREADS), 1) row_kernel(RowParams p) {
@@ -669,8 +671,9 @@ __global__ void __launch_bounds__((RowCfg<K, P>::THREADS), 1) row_kernel(RowPara
     constexpr int QR = RowCfg<K, P>::QR;
     constexpr bool WV = RowCfg<K, P>::kWave;
     // wave-shuffle pair: lane bit 0 selects the row of the pair, t per fft_shuffle.hpp
-    constexpr bool SHUF =
-        kShuffle<K, P> && (MODE == ROW_GS_MAIN || MODE == ROW_GD_MAIN || MODE == ROW_GD_LIN) && RPW == 2 && L == 1;
+    constexpr bool SHUF = kShuffle<K, P> &&
+                          (MODE == ROW_GS_MAIN || (P == PREC_F32 && (MODE == ROW_GD_MAIN || MODE == ROW_GD_LIN))) &&
+                          RPW == 2 && L == 1;
     int t, lrow;
     if constexpr (SHUF) {
         t = shuffle_t(threadIdx.x);
@@ -693,9 +696,9 @@ __global__ void __launch_bounds__((RowCfg<K, P>::THREADS), 1) row_kernel(RowPara
     Twiddles<K, C, tw_mode<P, RowCfg<K, P>::THREADS, K, false>()> tw;
     static_assert(!SHUF || (std::is_same_v<X, float2> && sizeof(smem) >= 4 * kShufN * sizeof(float2)),
                   "the shuffle pair needs two 2-line complex64 exchange buffers");
-    ShuffleTw stw;
+    ShuffleTwT<C> stw;
     if constexpr (SHUF)
-        load_shuffle_tw(stw, threadIdx.x, static_cast<const float2*>(p.tw) + twiddle_count_key(K));
+        load_shuffle_tw(stw, threadIdx.x, static_cast<const C*>(p.tw) + twiddle_count_key(K));
     else
         load_twiddles<K, C>(tw, t, p.tw);
 
@@ -991,8 +994,8 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), 1) col_kernel(ColPar
     // wave-shuffle pair: lane bit 0 selects the column (as here), t per fft_shuffle.hpp
     // (the GS and GD iteration modes)
     constexpr bool SHUF = kShuffle<K, P> && CW == 2 && L == 1 &&
-                          (MODE == COL_GS_MAIN || MODE == COL_GD_STATS || MODE == COL_GD_GRAD ||
-                           MODE == COL_GD_FUSED || MODE == COL_GD_LIN);
+                          (MODE == COL_GS_MAIN || (P == PREC_F32 && (MODE == COL_GD_STATS || MODE == COL_GD_GRAD ||
+                                                                      MODE == COL_GD_FUSED || MODE == COL_GD_LIN)));
     const int c = (threadIdx.x % (CW / L)) * L;
     const int t = SHUF ? shuffle_t(threadIdx.x) : threadIdx.x / (CW / L);
     // inputs (X, target) in layout X, outputs (Y) in layout Y: row y = t + T m
@@ -1012,9 +1015,9 @@ __global__ void __launch_bounds__((ColCfg<K, CW>::THREADS), 1) col_kernel(ColPar
     Twiddles<K, C, tw_mode<P, THREADS, K, true, L>()> tw;
     static_assert(!SHUF || (std::is_same_v<X, float2> && sizeof(smem) >= 4 * kShufN * sizeof(float2)),
                   "the shuffle pair needs two 2-line complex64 exchange buffers");
-    ShuffleTw stw;
+    ShuffleTwT<C> stw;
     if constexpr (SHUF)
-        load_shuffle_tw(stw, threadIdx.x, static_cast<const float2*>(p.tw) + twiddle_count_key(K));
+        load_shuffle_tw(stw, threadIdx.x, static_cast<const C*>(p.tw) + twiddle_count_key(K));
     else
         load_twiddles<K, C>(tw, t, p.tw);
     constexpr bool kTarget = (MODE == COL_GS_MAIN || MODE == COL_GD_STATS || MODE == COL_GD_GRAD ||

@@ -49,11 +49,11 @@ constexpr int kMaxRadix = 13;
 // LDS of one tile: at most this many complex128 elements (72 KiB: two
 // workgroups per CU); a single line may take up to kMaxLine (one per CU)
 constexpr int kTileElems = 4608;
-// radices above 8 (7, 11, 13) cost registers in every pass of a kernel that
-// can run them (generic odd DFTs): plans without them take kernels built for
-// radix <= 8 only (60-85 VGPRs, five 4-wave workgroups per CU) and plans with
-// them the full set (<= 128 VGPRs, four)
-constexpr int kMaxSmallRadix = 8;
+// the odd radices 7, 11, 13 (generic odd DFTs) cost registers in every pass
+// of a kernel that can run them: plans made of 2, 3, 4, 5 and 8 only take
+// kernels built for those (60-85 VGPRs, five 4-wave workgroups per CU), plans
+// with any other radix the full set (<= 128 VGPRs, four)
+__host__ __device__ constexpr bool small_radix(int r) { return r == 2 || r == 3 || r == 4 || r == 5 || r == 8; }
 constexpr int kMaxLine = 8192;
 
 // one line length's plan: radices in DIF stage order, the twiddle table
@@ -321,7 +321,7 @@ struct ColArgs {
     LinePlan pl;                       // length H
 };
 
-// host launchers (mr_inst.hip; big: a plan radix above kMaxSmallRadix; lds =
+// host launchers (mr_inst.hip; big: a plan radix that is not small_radix; lds =
 // tile elements x 16 B; 0 or -1 on a launch error)
 int mr_row_launch(int op, bool big, const RowArgs& a, int grid, size_t lds, hipStream_t st);
 int mr_col_launch(int op, bool big, const ColArgs& a, int grid, size_t lds, hipStream_t st);

@@ -297,6 +297,9 @@ struct slm_plan {
     long long holo = 0;
     hipStream_t stream = nullptr;
     int prec = PREC_F32;  // butterflies/twiddles; parity at both precisions: tests/test_gpu_precision.py
+    // row kernels' precision: prec, unless $SLM_ROW_PRECISION (f32 / f64, read at
+    // creation) splits the two kernels (A/B of float64 in one pass only)
+    int prec_row = PREC_F32, prec_row_force = -1;
     // write-through field stores per pass ($SLM_WT=0/1 forces both). Measured
     // (float32): write-through is faster for single images up to 1024^2 (no
     // dirty L2 at the kernel boundary); columns of 2048+ (2-column tiles:
@@ -450,12 +453,13 @@ int pick_plan(int n, long long elems, int prec, bool row = false) {
 // (slm_plan_create, slm_plan_set_precision).
 int configure(slm_plan* p, int prec) {
     const long long elems = (long long)p->B * p->holo;
-    const int row_key = pick_plan(p->W, elems, prec, true);
+    const int prow = p->prec_row_force >= 0 ? p->prec_row_force : prec;
+    const int row_key = pick_plan(p->W, elems, prow, true);
     const int col_key = pick_plan(p->H, elems, prec);
     const int cw = pick_cw(col_key, p->W);
     if (!cw) return fail(SLM_ERR_UNSUPPORTED, "no column tiling for %dx%d", p->H, p->W);
     const void *tr = nullptr, *tc = nullptr;
-    RC(get_twiddles(row_key, prec, &tr));
+    RC(get_twiddles(row_key, prow, &tr));
     RC(get_twiddles(col_key, prec, &tc));
     if (p->gexec) {  // the captured run bakes in kernels and tables
         HIP_TRY(hipStreamSynchronize(p->stream));  // a queued replay still owns the exec
@@ -473,7 +477,7 @@ int configure(slm_plan* p, int prec) {
     // keeps the default pair for GD only)
     const char* gl = std::getenv("SLM_GD_LAYOUT");
     const bool algo_ok = p->algo == SLM_ALGO_GS || !(gl && !std::strcmp(gl, "default"));
-    const bool narrow_ok = algo_ok && row_fn(row_key, ROW_GS_MAIN, prec, LAYOUT_NARROW) &&
+    const bool narrow_ok = algo_ok && row_fn(row_key, ROW_GS_MAIN, prow, LAYOUT_NARROW) &&
                            col_fn(col_key, cw, COL_GS_MAIN, TGT_AMP, prec, LAYOUT_NARROW);
     const char* ls = std::getenv("SLM_LAYOUT");
     if (narrow_ok && !(ls && !std::strcmp(ls, "default"))) lid = LAYOUT_NARROW;
@@ -484,13 +488,14 @@ int configure(slm_plan* p, int prec) {
     }
     p->lid = lid;
     p->prec = prec;
+    p->prec_row = prow;
     p->row_key = row_key;
     p->col_key = col_key;
     p->cw = cw;
     p->nwg = p->W / cw;
     p->col_threads = col_threads(col_key, cw);
-    p->row_threads = row_threads(row_key, prec);
-    p->rpw = row_rpw(row_key, prec);
+    p->row_threads = row_threads(row_key, prow);
+    p->rpw = row_rpw(row_key, prow);
     p->tw_row = tr;
     p->tw_col = tc;
     return 0;
@@ -567,7 +572,7 @@ int tile_grid(long long tiles, int* grid) {
 }
 
 int launch_row(slm_plan* p, int mode, const RowParams& rp, int cls) {
-    RowFn fn = row_fn(p->row_key, mode, p->prec, p->lid);
+    RowFn fn = row_fn(p->row_key, mode, p->prec_row, p->lid);
     if (!fn) return fail(SLM_ERR_UNSUPPORTED, "no row kernel for width %d mode %d", p->W, mode);
     RowParams r = rp;
     r.B = p->B;
@@ -1038,6 +1043,8 @@ int plan_create_on(int device, int algo, int batch, int height, int width, int t
     if (p->gd_mode == GD_TWO || p->gd_mode == GD_LIN) p->gd_fuse = 0;
     if (const char* e = std::getenv("SLM_GD_FAULT_TEST")) p->skip_wg_plus1 = std::atoi(e);
     if (const char* e = std::getenv("SLM_PRECISION")) p->prec = (std::strcmp(e, "f64") == 0) ? PREC_F64 : PREC_F32;
+    if (const char* e = std::getenv("SLM_ROW_PRECISION"))
+        p->prec_row_force = (std::strcmp(e, "f64") == 0) ? PREC_F64 : PREC_F32;
     // buffers indexed by column panel / row group hold the finer tiling of both precisions
     int max_nwg = 0, min_rpw = INT_MAX;
     if (generic) {
@@ -1471,11 +1478,12 @@ int slm_plan_engine(slm_plan* p, int* col_engine, int* row_engine) {
         *col_engine = *row_engine = generic_uses_blas(p->gen) ? 2 : 3;  // DFT-GEMM / mixed radix (generic.hpp)
         return 0;
     }
-    auto shuf = [&](int key) {
-        return p->prec == PREC_F32 && key >= 0 && kPlans[key].n == kShufN && kPlans[key].e == 8;
+    auto shuf = [&](int key, int prec) {
+        return (prec == PREC_F32 || p->algo == SLM_ALGO_GS) && key >= 0 && kPlans[key].n == kShufN &&
+               kPlans[key].e == 8;
     };
-    *col_engine = shuf(p->col_key) && p->cw == 2 ? 1 : 0;
-    *row_engine = shuf(p->row_key) && p->rpw == 2 ? 1 : 0;
+    *col_engine = shuf(p->col_key, p->prec) && p->cw == 2 ? 1 : 0;
+    *row_engine = shuf(p->row_key, p->prec_row) && p->rpw == 2 ? 1 : 0;
     return 0;
 }
 

@@ -228,7 +228,8 @@ def test_generic_incoming_amplitude_gs_and_gd(gpu, engine):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shape", [(1080, 1920), (1, 13), (26, 1), (77, 45), (1280, 1024), (8, 8192)])
+@pytest.mark.parametrize("shape", [(1080, 1920), (1, 13), (26, 1), (77, 45), (1280, 1024), (8, 8192), (14, 35),
+                                   (49, 20), (121, 169)])
 def test_mixed_radix_fft2_c128_vs_numpy(gpu, shape):
     """slm_fft2_c128 (float64 in and out) on the mixed-radix kernels, every
     radix and the ragged / degenerate tiles, against numpy.fft at float64
