@@ -53,6 +53,7 @@ struct GenericEngine {
     int cw_log2 = 0;         // columns per column tile = 2^cw_log2
     int nwg_col = 0;         // column tiles per hologram
     std::vector<void*> tables;  // device twiddle / reversal tables
+    float* ain_rev = nullptr;   // a_in with rows in the row transform's digit-reversed order (has_ain)
     // DFT-GEMM back end
     rocblas_handle blas = nullptr;
     double2* fh = nullptr;   // F_H [H][H]
@@ -146,6 +147,31 @@ __global__ void __launch_bounds__(kGT) k_c64_to_c128(const float2* in, double2* 
 __global__ void __launch_bounds__(kGT) k_c128_to_c64(const double2* in, float2* out, long long n) {
     for (long long i = blockIdx.x * (long long)kGT + threadIdx.x; i < n; i += (long long)gridDim.x * kGT)
         out[i] = make_float2((float)in[i].x, (float)in[i].y);
+}
+// Mixed-radix GD keeps its field x with every row in the digit-reversed order
+// of the row transform (element e of a row holds column rev[e]: the row pass
+// reads and writes it in place, coalesced); these read it back row-major.
+__global__ void __launch_bounds__(kGT) k_phase_rev(const double2* X, float* phase, const int* rev, int W, long long n) {
+    for (long long i = blockIdx.x * (long long)kGT + threadIdx.x; i < n; i += (long long)gridDim.x * kGT) {
+        const long long r = i / W;
+        const int e = (int)(i - r * W);
+        phase[r * W + rev[e]] = (float)atan2(X[i].y, X[i].x);
+    }
+}
+__global__ void __launch_bounds__(kGT) k_c128_to_c64_rev(const double2* X, float2* out, const int* rev, int W,
+                                                        long long n) {
+    for (long long i = blockIdx.x * (long long)kGT + threadIdx.x; i < n; i += (long long)gridDim.x * kGT) {
+        const long long r = i / W;
+        const int e = (int)(i - r * W);
+        out[r * W + rev[e]] = make_float2((float)X[i].x, (float)X[i].y);
+    }
+}
+// a_in [H][W] with every row in that order (read by the iteration row passes)
+__global__ void __launch_bounds__(kGT) k_ain_rev(const float* ain, float* out, const int* rev, int W, long long n) {
+    for (long long i = blockIdx.x * (long long)kGT + threadIdx.x; i < n; i += (long long)gridDim.x * kGT) {
+        const long long r = i / W;
+        out[i] = ain[r * W + rev[(int)(i - r * W)]];
+    }
 }
 __global__ void __launch_bounds__(kGT) k_phase(const double2* A, float* phase, long long n) {
     for (long long i = blockIdx.x * (long long)kGT + threadIdx.x; i < n; i += (long long)gridDim.x * kGT)
@@ -499,6 +525,7 @@ int mr_row(GenericEngine* g, const GenericView& v, int op, mr::RowArgs a, int cl
     a.holo = v.holo;
     a.inv_s = 1.0 / (double)v.holo;
     a.ain = v.ain;
+    a.ain_rev = v.ain ? g->ain_rev : nullptr;
     a.stop = v.stop;
     const int grid = v.B * ((v.H + g->rpw - 1) / g->rpw);
     const size_t lds = (size_t)g->rpw * v.W * sizeof(double2);
@@ -554,6 +581,9 @@ int mr_enqueue(GenericEngine* g, const GenericView& v, int loops, double tol, in
     mr::ColArgs c;
     r.checked = c.checked = checked;
     c.wa = wa;
+    if (v.ain)  // the row passes read a_in in their digit-reversed order
+        hipLaunchKernelGGL(k_ain_rev, dim3(grid_of(v.holo)), dim3(kGT), 0, st, v.ain, g->ain_rev, g->pw.rev, v.W,
+                           v.holo);
     if (v.algo == SLM_ALGO_GS) {
         // setup (src/algorithms.py:14-27): the warm start B = a_in exp(i phi), or
         // A0 = ifft2(sqrt T) in complex64, B = a_in A0/|A0|; row-transformed into a
@@ -613,7 +643,7 @@ int mr_enqueue(GenericEngine* g, const GenericView& v, int loops, double tol, in
             r.last = i + 1 == loops;
             if (int rc = mr_row(g, v, mr::RO_GD, r, SLM_KERNEL_ROW_MAIN)) return rc;
         }
-        hipLaunchKernelGGL(k_phase, dim3(grid), dim3(kGT), 0, st, g->x, v.phase_out, n);
+        hipLaunchKernelGGL(k_phase_rev, dim3(grid), dim3(kGT), 0, st, g->x, v.phase_out, g->pw.rev, v.W, n);
     }
     G_HIP(hipGetLastError());
     return 0;
@@ -637,6 +667,7 @@ void generic_destroy(GenericEngine* g) {
         if (p) (void)hipFree(p);
     for (void* p : g->tables)
         if (p) (void)hipFree(p);
+    if (g->ain_rev) (void)hipFree(g->ain_rev);
     if (g->fh && g->fh != g->fw) (void)hipFree(g->fh);
     if (g->blas) (void)rocblas_destroy_handle(g->blas);
     delete g;
@@ -661,7 +692,8 @@ int generic_create(const GenericView& v, GenericEngine** out) {
         g->nwg_col = (v.W + (1 << g->cw_log2) - 1) >> g->cw_log2;
         g->rpw = t.rpw;
         if (g->nwg_col != v.nwg) return fail_free(slm_set_error(SLM_ERR_STATE, "mixed radix: partial-slab mismatch"));
-        if (!alloc(&g->a, n) || !alloc(&g->b, n) || (v.algo == SLM_ALGO_GD && !alloc(&g->x, n)))
+        if (!alloc(&g->a, n) || !alloc(&g->b, n) || (v.algo == SLM_ALGO_GD && !alloc(&g->x, n)) ||
+            (v.has_ain && hipMalloc((void**)&g->ain_rev, (size_t)v.holo * sizeof(float)) != hipSuccess))
             return fail_free(slm_set_error(SLM_ERR_HIP, "mixed radix: device allocation failed"));
         if (int rc = mr_plan_line(g, v.W, &g->pw, v.stream)) return fail_free(rc);
         if (int rc = mr_plan_line(g, v.H, &g->ph, v.stream)) return fail_free(rc);
@@ -758,7 +790,10 @@ int generic_enqueue(GenericEngine* g, const GenericView& v, int loops, double to
 int generic_field(GenericEngine* g, const GenericView& v, float2* out) {
     if (!g->x) return slm_set_error(SLM_ERR_STATE, "the field is the state of GD plans");
     const long long n = (long long)v.B * v.holo;
-    hipLaunchKernelGGL(k_c128_to_c64, dim3(grid_of(n)), dim3(kGT), 0, v.stream, g->x, out, n);
+    if (g->mr)  // rows in digit-reversed order
+        hipLaunchKernelGGL(k_c128_to_c64_rev, dim3(grid_of(n)), dim3(kGT), 0, v.stream, g->x, out, g->pw.rev, v.W, n);
+    else
+        hipLaunchKernelGGL(k_c128_to_c64, dim3(grid_of(n)), dim3(kGT), 0, v.stream, g->x, out, n);
     G_HIP(hipGetLastError());
     return 0;
 }

@@ -292,9 +292,10 @@ struct RowArgs {
     const double2* in = nullptr;
     double2* out = nullptr;
     const float* ain = nullptr;        // [H][W] or nullptr (uniform)
+    const float* ain_rev = nullptr;    // the same with rows in digit-reversed order (DIF side)
     const float* phase_in = nullptr;   // RO_WARM
     float* phase_out = nullptr;        // RO_GS
-    double2* x = nullptr;              // GD state
+    double2* x = nullptr;              // GD state, rows in digit-reversed order (element e = column rev[e])
     const float2* field0 = nullptr;    // RO_GD_INIT
     const float* lr = nullptr;         // RO_GD, per iteration
     const int* stop = nullptr;         // [B]

@@ -68,6 +68,8 @@ __global__ void __launch_bounds__(kThreads, kWavesPerSimd<BIG>) mr_row_kernel(Ro
         return r * W + rev[e - r * W];
     };
     auto ain = [&](int px) -> double { return a.ain ? (double)a.ain[pix0 + px] : 1.0; };
+    // a_in at tile position e on the digit-reversed side (rows in that order)
+    auto ain_e = [&](int e) -> double { return a.ain_rev ? (double)a.ain_rev[pix0 + e] : 1.0; };
     constexpr bool GATHER = OP == RO_FWD || OP == RO_INV || OP == RO_WARM || OP == RO_GD_INIT;
     for (int e = threadIdx.x; e < ne; e += kThreads) {
         double2 v;
@@ -80,9 +82,10 @@ __global__ void __launch_bounds__(kThreads, kWavesPerSimd<BIG>) mr_row_kernel(Ro
                 const double am = ain(px);
                 v = make_double2((double)(float)c * am, (double)(float)s * am);
             } else if constexpr (OP == RO_GD_INIT) {
+                // x keeps each row in digit-reversed order: the GD row pass reads it in place
                 const float2 f = a.field0[off + px];
                 const double2 x = make_double2((double)f.x, (double)f.y);
-                a.x[off + px] = x;
+                a.x[off + e] = x;
                 v = u_of(x, ain(px));
             } else {
                 v = a.in[off + px];
@@ -102,37 +105,36 @@ __global__ void __launch_bounds__(kThreads, kWavesPerSimd<BIG>) mr_row_kernel(Ro
         const bool phase_only = OP == RO_GS && (a.last || (a.checked && a.stop[b] == a.iter));
         const double l = OP == RO_GD ? (double)a.lr[a.iter] : 0.0;
         for (int e = threadIdx.x; e < ne; e += kThreads) {
-            const int px = nat(e);
             const double2 z = lds[e];
             if constexpr (OP == RO_COLD) {
-                lds[e] = unit_of(round_c64(z), ain(px));  // A0 = ifft2(sqrt T) is complex64 (:27)
+                lds[e] = unit_of(round_c64(z), ain_e(e));  // A0 = ifft2(sqrt T) is complex64 (:27)
             } else if constexpr (OP == RO_GS) {
                 if (phase_only)
-                    a.phase_out[off + px] = (float)atan2(z.y, z.x);  // hologram = np.angle(A) (:48)
+                    a.phase_out[off + nat(e)] = (float)atan2(z.y, z.x);  // hologram = np.angle(A) (:48)
                 else
-                    lds[e] = unit_of(z, ain(px));
+                    lds[e] = unit_of(z, ain_e(e));
             } else if constexpr (OP == RO_GD_FOURIER) {
                 // angle of the complex64 ifft2 is float32, exp of it complex64 (:153-156)
                 const double2 c = round_c64(z);
                 const float ang = atan2f((float)c.y, (float)c.x);
                 double s, co;
                 sincos((double)ang, &s, &co);
-                const double am = ain(px);
+                const double am = ain_e(e);
                 const double2 x = make_double2((double)(float)co * am, (double)(float)s * am);
-                a.x[off + px] = x;
+                a.x[off + e] = x;
                 lds[e] = u_of(x, am);
             } else if constexpr (OP == RO_GD) {
                 // dEdF = ifft2(G) a_in (unscaled transform * 1/S), dEdX_complex, x -= lr dEdX
-                const double am = ain(px);
+                const double am = ain_e(e);
                 const double s = am * a.inv_s;
                 const double gx = z.x * s, gy = z.y * s;
-                double2 x = a.x[off + px];
+                double2 x = a.x[off + e];
                 const double ax2 = x.x * x.x + x.y * x.y;
                 const double ax = sqrt(ax2);
                 const double re = x.x * gx + x.y * gy;
                 x.x -= l * ((gx - x.x * (re / ax2)) / ax);
                 x.y -= l * ((gy - x.y * (re / ax2)) / ax);
-                a.x[off + px] = x;
+                a.x[off + e] = x;
                 lds[e] = u_of(x, am);
             }
         }
