@@ -406,8 +406,10 @@ bool mr_big(int H, int W) {
 // per CU in a round) x e: so the rows per row tile / columns per column tile
 // minimise ceil(wgs / (cus occ)) * min(occ, ceil(wgs / cus)) * e (a grid one
 // workgroup too large for a round doubles the launch: 1080 rows in 540
-// two-row tiles on 512 slots did, 62.6 against ~35 us). Ties go to the wider
-// tile (longer contiguous HBM segments). $SLM_MR_RPW / $SLM_MR_CW override.
+// two-row tiles on 512 slots did, 62.6 against ~35 us). Ties go to the
+// narrower column tile (more workgroups per CU: 1080 x 1920 columns of 2
+// measured 48.1 us against 54.5 us in tiles of 4, profiles/r05) and to the
+// wider row tile. $SLM_MR_RPW / $SLM_MR_CW override.
 struct MrTiling {
     int rpw = 1, cw_log2 = 0;
 };
@@ -441,7 +443,7 @@ MrTiling mr_tiling(int B, int H, int W) {
         const int occ = mr::mr_col_occupancy(mr::CO_GS, big, ((size_t)H << c) * sizeof(double2));
         if (occ < 1) continue;
         const long long v = cost((long long)B * ((W + (1 << c) - 1) >> c), occ, (long long)H << c);
-        if (best < 0 || v <= best) {
+        if (best < 0 || v < best) {
             best = v;
             t.cw_log2 = c;
         }

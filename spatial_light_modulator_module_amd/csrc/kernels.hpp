@@ -331,6 +331,18 @@ __device__ __forceinline__ C normalize(C x, Scalar<C> a) {
     return mk<C>(x.x * r * a, x.y * r * a);
 }
 
+// Lane i <- lane i ^ 4 within each 16-lane DPP row (row_ror:4 moves lane i - 4
+// into lane i, row_ror:12 lane i + 4; lanes with bit 2 set take the first)
+__device__ __forceinline__ float lane_xor4(float x, bool b2) {
+    const int v = __builtin_bit_cast(int, x);
+    const int dn = __builtin_amdgcn_update_dpp(0, v, 0x124, 0xF, 0xF, false);
+    const int up = __builtin_amdgcn_update_dpp(0, v, 0x12C, 0xF, 0xF, false);
+    return __builtin_bit_cast(float, b2 ? dn : up);
+}
+__device__ __forceinline__ float2 lane_xor4(float2 z, bool b2) {
+    return make_float2(lane_xor4(z.x, b2), lane_xor4(z.y, b2));
+}
+
 // Field stores of the iteration passes. wt = write-through (agent-scope
 // relaxed atomic store = global_store sc1): the bytes go to memory as they are
 // stored, so the kernel ends with no dirty L2 lines to write back before the
@@ -674,6 +686,16 @@ __global__ void __launch_bounds__((RowCfg<K, P>::THREADS), 1) row_kernel(RowPara
     constexpr bool SHUF = kShuffle<K, P> &&
                           (MODE == ROW_GS_MAIN || (P == PREC_F32 && (MODE == ROW_GD_MAIN || MODE == ROW_GD_LIN))) &&
                           RPW == 2 && L == 1;
+    // Row pairs in 4-wide panels (the float32 4096 rows): a row pair's piece of
+    // a panel is one 64-B sector (4 columns x 2 rows). Lanes t and t ^ 4 swap
+    // halves (lane_xor4) so that each load / store instruction moves whole
+    // sectors -- lanes with t bit 2 clear the row-r halves of panel t / 4, the
+    // others the row-(r+1) halves of the same panel -- instead of every
+    // instruction writing half of each sector of one row (r04: 1.145x write and
+    // 1.15x read traffic per 8 x 4096^2 row pass in partly merged sectors,
+    // TCC_EA0_WRREQ_64B = all write requests, profiles/r05).
+    constexpr bool kSector = L == 2 && kPanelOf<LAYOUT_X> == 4 && kPanelOf<LAYOUT_Y> == 4 && !SHUF &&
+                             !RowCfg<K, P>::kRemap && RowCfg<K, P>::RL == 1 && T % 8 == 0 && std::is_same_v<V, float2>;
     int t, lrow;
     if constexpr (SHUF) {
         t = shuffle_t(threadIdx.x);
@@ -738,7 +760,20 @@ __global__ void __launch_bounds__((RowCfg<K, P>::THREADS), 1) row_kernel(RowPara
                     v[l][m] = cv<V>(normalize(from_c64<C>(p.field_src[boff + PY * l + m * bstep]), ain_at(l, m)));
             }
         }
-        if constexpr (MODE != ROW_PHASE_FWD && MODE != ROW_GD_INIT_FIELD) {
+        if constexpr (MODE != ROW_PHASE_FWD && MODE != ROW_GD_INIT_FIELD && kSector) {
+            // whole 64-B sectors per instruction: lane bit 2 clear loads (r, t) and
+            // (r, t ^ 4), set (r + 1, t ^ 4) and (r + 1, t); one lane_xor4 restores
+            const bool b2 = (t >> 2) & 1;
+            const long long o1 = b2 ? PY - 4LL * p.H : 0, o2 = b2 ? PY : 4LL * p.H;
+#pragma unroll
+            for (int m = 0; m < E; ++m) {
+                const float2 l1 = p.in[boff + o1 + m * bstep];
+                const float2 l2 = p.in[boff + o2 + m * bstep];
+                const float2 r = lane_xor4(b2 ? l1 : l2, b2);
+                v[0][m] = b2 ? r : l1;
+                v[1][m] = b2 ? l2 : r;
+            }
+        } else if constexpr (MODE != ROW_PHASE_FWD && MODE != ROW_GD_INIT_FIELD) {
 #pragma unroll
             for (int m = 0; m < E; ++m)  // slot-major, as the stores
 #pragma unroll
@@ -872,7 +907,24 @@ __global__ void __launch_bounds__((RowCfg<K, P>::THREADS), 1) row_kernel(RowPara
         // of one 128-B line leave back to back (tools/row_store_probe.hip, a copy of
         // 8 x 4096^2 in the row pass's shapes: 32-B row pieces 711 us, adjacent row
         // pairs 531 us, whole lines 445 us)
-        if (p.wt) {  // uniform: one branch per tile, not per store
+        if constexpr (kSector) {
+            // whole 64-B sectors per instruction (the loads' exchange, reversed)
+            const bool b2 = (t >> 2) & 1;
+            const long long o1 = b2 ? PX - 4LL * p.H : 0, o2 = b2 ? PX : 4LL * p.H;
+            auto sectors = [&](auto wtc) {
+#pragma unroll
+                for (int m = 0; m < E; ++m) {
+                    const float2 a = cv<float2>(v[0][m]), c = cv<float2>(v[1][m]);
+                    const float2 r = lane_xor4(b2 ? a : c, b2);
+                    store_field(p.out + xoff + o1 + m * bstep, b2 ? r : a, decltype(wtc)::value);
+                    store_field(p.out + xoff + o2 + m * bstep, b2 ? c : r, decltype(wtc)::value);
+                }
+            };
+            if (p.wt)  // uniform: one branch per tile, not per store
+                sectors(std::integral_constant<int, 1>{});
+            else
+                sectors(std::integral_constant<int, 0>{});
+        } else if (p.wt) {  // uniform: one branch per tile, not per store
 #pragma unroll
             for (int m = 0; m < E; ++m)
 #pragma unroll

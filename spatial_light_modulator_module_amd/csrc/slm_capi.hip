@@ -1810,6 +1810,42 @@ int gather_slab(slm_plan* p, const void* src, long long per_item, size_t elem, n
     if (p->fused_pending) RC(slm_plan_sync(p));
     std::vector<long long> off(n + 1);
     RC(slm_gather_layout(n, counts, per_item, off.data()));
+    static const bool staged = [] {  // $SLM_GATHER_STAGED=0: r04's gather on the plan stream (A/B)
+        const char* e = std::getenv("SLM_GATHER_STAGED");
+        return !e || std::atoi(e) != 0;
+    }();
+    if (!staged) {
+        if (me == root) {
+            const long long elems = off[n];
+            if (*dev_cap < elems) {
+                HIP_TRY(hipStreamSynchronize(p->stream));
+                if (*dev_buf) HIP_TRY(hipFree(*dev_buf));
+                *dev_buf = nullptr;
+                *dev_cap = 0;
+                HIP_TRY(hipMalloc(dev_buf, std::max<long long>(elems, 1) * elem));
+                *dev_cap = elems;
+            }
+            char* dst = static_cast<char*>(*dev_buf);
+            if (n > 1) NCCL_TRY(ncclGroupStart());
+            for (int r = 0; r < n; ++r) {
+                const size_t cnt = (size_t)(off[r + 1] - off[r]);
+                if (!cnt) continue;
+                if (r == me)
+                    HIP_TRY(hipMemcpyAsync(dst + off[r] * elem, src, cnt * elem, hipMemcpyDeviceToDevice, p->stream));
+                else
+                    NCCL_TRY(ncclRecv(dst + off[r] * elem, cnt, dt, r, g_comm, p->stream));
+            }
+            if (n > 1) NCCL_TRY(ncclGroupEnd());
+            if (host_out && elems) {
+                HIP_TRY(hipStreamSynchronize(p->stream));
+                RC(copy_sync(host_out, dst, (size_t)elems * elem, hipMemcpyDeviceToHost, p->stream));
+            }
+        } else {
+            if (!g_comm) return fail(SLM_ERR_COMM, "no communicator");
+            if (p->B) NCCL_TRY(ncclSend(src, (size_t)p->B * per_item, dt, root, g_comm, p->stream));
+        }
+        return 0;
+    }
     if (!p->comm_stream) {
         HIP_TRY(hipStreamCreateWithFlags(&p->comm_stream, hipStreamNonBlocking));
         HIP_TRY(hipEventCreateWithFlags(&p->gather_ready, hipEventDisableTiming));

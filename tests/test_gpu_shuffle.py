@@ -52,16 +52,18 @@ def test_shuffle_model():
 
 @pytest.mark.gpu
 def test_engine_selection(gpu):
-    """GS and GD float32 plans with 1024-point narrow lines run the shuffle
-    pair on that axis; float64 butterflies and the wide batched plan keep the
-    Stockham pair."""
+    """GS and GD float32 plans and GS float64 plans with 1024-point narrow
+    lines run the shuffle pair on that axis (float64: double values between
+    its passes, r05); GD float64 and the wide batched plan keep the Stockham
+    pair."""
     lib = gpu
     cases = [
         ((1, 1024, 1024), lib.ALGO_GS, lib.PRECISION_F32, ("shuffle", "shuffle")),
         ((2, 1024, 1024), lib.ALGO_GS, lib.PRECISION_F32, ("shuffle", "shuffle")),
         ((1, 768, 1024), lib.ALGO_GS, lib.PRECISION_F32, ("stockham", "shuffle")),
         ((1, 1024, 768), lib.ALGO_GS, lib.PRECISION_F32, ("shuffle", "stockham")),
-        ((1, 1024, 1024), lib.ALGO_GS, lib.PRECISION_F64, ("stockham", "stockham")),
+        ((1, 1024, 1024), lib.ALGO_GS, lib.PRECISION_F64, ("shuffle", "shuffle")),
+        ((1, 1024, 1024), lib.ALGO_GD, lib.PRECISION_F64, ("stockham", "stockham")),
         ((1, 1024, 1024), lib.ALGO_GD, lib.PRECISION_F32, ("shuffle", "shuffle")),
         ((64, 1024, 1024), lib.ALGO_GS, lib.PRECISION_F32, ("stockham", "stockham")),
     ]

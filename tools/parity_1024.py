@@ -30,8 +30,7 @@ def run(t, phi_w, span, cfg):
     else:
         os.environ.pop("SLM_ROW_PRECISION", None)
     with _lib.Plan(_lib.ALGO_GS, 1, 1024, 1024, _lib.TGT_F32, False, span) as p:
-        if env[0] is None:
-            p.set_precision(env[1])
+        p.set_precision(env[1])  # the column kernels' (and, without the override, the rows') precision
         p.set_target(t[None])
         p.set_phase(np.asarray(phi_w, np.float32)[None])
         p.run(span)
