@@ -56,21 +56,30 @@ __global__ void __launch_bounds__(256) field_phase_kernel(const float2* field, f
 // 6 % active, r04). AMP: the upload of a float32 GS target stores its
 // amplitude sqrt(T) (TgtLoad<TGT_F32>::amp; TGT_AMP device targets).
 //
-// LDS: tile rows of 64 WV words (WV = 32-bit words per element) at a stride of
-// 64 WV + 4 words, written and read as 16-B (or P WV-word) pieces: a 16-lane
-// group of ds_write_b128 / ds_read_b128 down one panel column touches 16 rows
-// = 16 distinct 4-bank groups (no conflicts; MI355X_MICROARCH.md, LDS banks).
+// LDS: tile rows of 64 WV words, unpadded, with the 16-B chunks of row y
+// XOR-swizzled by g(y) = (y * PW / 4) mod 16 (PW / 4 = chunks per panel row;
+// (y / (4 / PW)) mod 16 for panel rows under 16 B), so that both the
+// row-major side (ds_read_b128 / ds_write_b128 along rows) and the blocked side
+// (16-lane groups walking down one panel column) hit distinct banks: the
+// bank model of tools/lds_bank_sim.py (MI355X_MICROARCH.md LDS table) gives 0
+// extra cycles per LDS instruction for every float / complex64 panel width but
+// float P = 2 (1.3 / 2.7) and float P = 16 from the blocked layout (2.0),
+// where r04's padded rows (LD = 64 WV + 4) cost 2.0 on the 4096^2 unblock
+// (measured SQ_LDS_BANK_CONFLICT / LDS instruction, profiles/r05/sq_4096x8_s7.txt).
 template <typename V, int PLOG, bool TO_BLOCKED, bool AMP = false>
 __global__ void __launch_bounds__(256) tile_relayout_kernel(const V* in, V* out, int H, int W) {
     static_assert(!AMP || sizeof(V) == 4, "the amplitude applies to float planes");
     constexpr int WV = sizeof(V) / 4;   // 32-bit words per element
     constexpr int P = 1 << PLOG;
     constexpr int RW = 64 * WV;         // words per tile row
-    constexpr int LD = RW + 4;          // LDS row stride (16-B aligned, 4-bank skew per row)
     constexpr int PW = P * WV;          // words of one panel row
     constexpr int BV = PW < 4 ? PW : 4; // words per LDS access on the blocked side
     constexpr int ROWS = 4 / BV;        // rows of one panel per 16-B blocked-side access
-    __shared__ __attribute__((aligned(16))) float tile[64 * LD];
+    __shared__ __attribute__((aligned(16))) float tile[64 * RW];
+    auto lds = [](int yy, int w) -> int {
+        const int g = PW >= 4 ? (yy * (PW / 4)) & 15 : (yy / (4 / (PW < 4 ? PW : 4))) & 15;
+        return yy * RW + ((((w >> 2) ^ g)) << 2) + (w & 3);
+    };
     const long long holo = (long long)H * W;
     const int x0 = blockIdx.x * 64, y0 = blockIdx.y * 64;
     const float* src = reinterpret_cast<const float*>(in + blockIdx.z * holo);
@@ -104,7 +113,7 @@ __global__ void __launch_bounds__(256) tile_relayout_kernel(const V* in, V* out,
                 v.z = TgtLoad<TGT_F32>::amp(v.z);
                 v.w = TgtLoad<TGT_F32>::amp(v.w);
             }
-            *reinterpret_cast<float4*>(tile + yy * LD + w) = v;
+            *reinterpret_cast<float4*>(tile + lds(yy, w)) = v;
         }
         __syncthreads();
         for (int i = threadIdx.x; i < N4; i += 256) {
@@ -114,7 +123,7 @@ __global__ void __launch_bounds__(256) tile_relayout_kernel(const V* in, V* out,
             float* pv = reinterpret_cast<float*>(&v);
 #pragma unroll
             for (int r = 0; r < ROWS; ++r) {
-                const float* t = tile + (yy + r) * LD + q * PW + w;
+                const float* t = tile + lds(yy + r, q * PW + w);
                 if constexpr (BV == 4) {
                     v = *reinterpret_cast<const float4*>(t);
                 } else if constexpr (BV == 2) {
@@ -135,7 +144,7 @@ __global__ void __launch_bounds__(256) tile_relayout_kernel(const V* in, V* out,
             const float* pv = reinterpret_cast<const float*>(&v);
 #pragma unroll
             for (int r = 0; r < ROWS; ++r) {
-                float* t = tile + (yy + r) * LD + q * PW + w;
+                float* t = tile + lds(yy + r, q * PW + w);
                 if constexpr (BV == 4) {
                     *reinterpret_cast<float4*>(t) = v;
                 } else if constexpr (BV == 2) {
@@ -150,7 +159,7 @@ __global__ void __launch_bounds__(256) tile_relayout_kernel(const V* in, V* out,
             int yy, w;
             rm_at(i, yy, w);
             *reinterpret_cast<float4*>(dst + (long long)(y0 + yy) * W * WV + (long long)x0 * WV + w) =
-                *reinterpret_cast<const float4*>(tile + yy * LD + w);
+                *reinterpret_cast<const float4*>(tile + lds(yy, w));
         }
     }
 }
