@@ -160,7 +160,9 @@ def rank_diagnostics(plan, counts, rank, local_elapsed, steps, rows):
     kern = {k: round(v["avg_us"], 3) for k, v in rows.items()}
     run_us = sum(v["total_us"] for v in rows.values())
     return {"rank": rank, "device": dev, "pci_bus_id": bus, "holograms": int(counts[rank]),
-            "gather_stream": "comm stream behind a staging copy (overlaps the next run)",
+            "gather_stream": ("comm stream behind a staging copy (overlaps the next run)"
+                              if os.environ.get("SLM_GATHER_STAGED", "0") not in ("", "0")
+                              else "plan stream (default; the staged comm-stream gather measured slower)"),
             "step_ms": round(local_elapsed / steps * 1e3, 4), "kernel_avg_us": kern,
             "iteration_kernels_ms_per_run": round(run_us / 1e3, 4),
             "gather_ms": round(gather_ms, 4), "gather_bytes_to_root": gather_bytes,

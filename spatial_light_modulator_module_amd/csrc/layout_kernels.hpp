@@ -63,7 +63,8 @@ __global__ void __launch_bounds__(256) field_phase_kernel(const float2* field, f
 // (16-lane groups walking down one panel column) hit distinct banks: the
 // bank model of tools/lds_bank_sim.py (MI355X_MICROARCH.md LDS table) gives 0
 // extra cycles per LDS instruction for every float / complex64 panel width but
-// float P = 2 (1.3 / 2.7) and float P = 16 from the blocked layout (2.0),
+// float P = 16 from the blocked layout (2.0; float P = 2 with the lane order
+// of `piece` below, 1.3 / 2.7 without),
 // where r04's padded rows (LD = 64 WV + 4) cost 2.0 on the 4096^2 unblock
 // (measured SQ_LDS_BANK_CONFLICT / LDS instruction, profiles/r05/sq_4096x8_s7.txt).
 template <typename V, int PLOG, bool TO_BLOCKED, bool AMP = false>
@@ -98,6 +99,13 @@ __global__ void __launch_bounds__(256) tile_relayout_kernel(const V* in, V* out,
         yy = r / PW;
         w = r - yy * PW;
     };
+    // blocked-side piece of loop index i: for 8-B panel rows (PW == 2) the
+    // lanes of a wave alternate between the two panels of its 1 KB (lane l
+    // takes piece 32 (l & 1) + l / 2), so a 16-lane LDS group writes / reads
+    // both 8-B halves of 8 chunks -- 16 distinct bank pairs -- instead of one
+    // half of 16 rows' chunks (2 / 4 of 8 bank pairs busy twice). The wave's
+    // global access still covers the same contiguous 1 KB.
+    auto piece = [](int i) { return PW == 2 ? (i & ~63) | ((i & 1) << 5) | ((i & 63) >> 1) : i; };
     auto gbl = [&](int q, int yy, int w) -> long long {
         return (((long long)(x0 >> PLOG) + q) * H + y0 + yy) * PW + w;
     };
@@ -118,7 +126,7 @@ __global__ void __launch_bounds__(256) tile_relayout_kernel(const V* in, V* out,
         __syncthreads();
         for (int i = threadIdx.x; i < N4; i += 256) {
             int q, yy, w;
-            bl_at(i, q, yy, w);
+            bl_at(piece(i), q, yy, w);
             float4 v;
             float* pv = reinterpret_cast<float*>(&v);
 #pragma unroll
@@ -139,7 +147,7 @@ __global__ void __launch_bounds__(256) tile_relayout_kernel(const V* in, V* out,
     } else {
         for (int i = threadIdx.x; i < N4; i += 256) {
             int q, yy, w;
-            bl_at(i, q, yy, w);
+            bl_at(piece(i), q, yy, w);
             const float4 v = *reinterpret_cast<const float4*>(src + gbl(q, yy, w));
             const float* pv = reinterpret_cast<const float*>(&v);
 #pragma unroll

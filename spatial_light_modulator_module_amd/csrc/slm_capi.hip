@@ -1790,11 +1790,13 @@ namespace {
 // Gather one per-hologram slab of every rank to `root` (rank order): `src`
 // holds this rank's counts[me] x per_item elements of `elem` bytes (RCCL type
 // `dt`); on root the concatenation lands in *dev_buf (grown as needed) and,
-// if host_out, on the host. The slab is first copied into a staging buffer on
-// the plan stream (so the next run, queued behind that copy, may overwrite
-// `src`), then the comm stream -- behind an event -- moves it: grouped
-// ncclSend / ncclRecv (one xGMI hop per peer), the root's own slab a device
-// copy. Stream-ordered, no host synchronisation unless host_out.
+// if host_out, on the host. Default: grouped ncclSend / ncclRecv (one xGMI
+// hop per peer) and the root's own slab as a device copy, on the plan stream.
+// Staged ($SLM_GATHER_STAGED=1): the slab is first copied into one of two
+// staging buffers on the plan stream (so the next run, queued behind that
+// copy, may overwrite `src`), then the comm stream -- behind an event -- moves
+// it, overlapping the next run. Stream-ordered either way, no host
+// synchronisation unless host_out.
 int gather_slab(slm_plan* p, const void* src, long long per_item, size_t elem, ncclDataType_t dt, const int* counts,
                 int root, void** dev_buf, long long* dev_cap, void* host_out) {
     if (!p || !counts) return fail(SLM_ERR_ARG, "null argument");
@@ -1810,11 +1812,17 @@ int gather_slab(slm_plan* p, const void* src, long long per_item, size_t elem, n
     if (p->fused_pending) RC(slm_plan_sync(p));
     std::vector<long long> off(n + 1);
     RC(slm_gather_layout(n, counts, per_item, off.data()));
-    static const bool staged = [] {  // $SLM_GATHER_STAGED=0: r04's gather on the plan stream (A/B)
-        const char* e = std::getenv("SLM_GATHER_STAGED");
-        return !e || std::atoi(e) != 0;
-    }();
+    // $SLM_GATHER_STAGED=1: stage the slab and move it on the plan's comm stream
+    // (overlaps the next run). Off by default: at 1024^2 the second stream cost
+    // 0.28 ms per 200-iteration run on one GPU (272-275 against 295-296
+    // holograms/s, profiles/r05/gather_ab_s7.txt), more than rank 0's wait for
+    // seven 4 MB receives is expected to cost. Read per call (tests switch it).
+    const char* st_env = std::getenv("SLM_GATHER_STAGED");
+    const bool staged = st_env && std::atoi(st_env) != 0;
     if (!staged) {
+        // a staged gather still queued on the comm stream may write the same buffer
+        if (p->gather_last >= 0) HIP_TRY(hipStreamWaitEvent(p->stream, p->gather_done[p->gather_last], 0));
+        p->gather_last = -1;
         if (me == root) {
             const long long elems = off[n];
             if (*dev_cap < elems) {

@@ -175,15 +175,27 @@ def test_multi_gpu_diagnostics(gpu):
 
 
 @pytest.mark.gpu
-def test_gather_overlaps_next_run_stream_ordered(gpu):
-    """The phase gather stages the slab on the plan stream and moves it on the
-    plan's comm stream (two staging buffers, used alternately), so the next
-    run is queued right behind the staging copy. Each gather must still carry
-    the phases of the run before it, bit for bit, whatever runs are queued
-    behind it and however the staging buffers alternate: run -> gather ->
-    run -> gather -> gather, with no host synchronisation in between until
-    the host copies (src/generate_hologram_sequence.py:19-31 is the loop)."""
+@pytest.mark.parametrize("staged", ["1", "0", "mixed"])
+def test_gather_overlaps_next_run_stream_ordered(gpu, monkeypatch, staged):
+    """Staged ($SLM_GATHER_STAGED=1): the phase gather stages the slab on the
+    plan stream and moves it on the plan's comm stream (two staging buffers,
+    used alternately), so the next run is queued right behind the staging
+    copy; default: the gather on the plan stream; mixed: the two alternate
+    (a plan-stream gather must wait for a staged one still queued). Each
+    gather must carry the phases of the run before it, bit for bit, whatever
+    runs are queued behind it and however the staging buffers alternate: run
+    -> gather -> run -> gather -> gather, with no host synchronisation in
+    between until the host copies (src/generate_hologram_sequence.py:19-31 is
+    the loop)."""
     lib = gpu
+    flip = [False]
+
+    def mode():
+        if staged == "mixed":
+            flip[0] = not flip[0]
+            monkeypatch.setenv("SLM_GATHER_STAGED", "1" if flip[0] else "0")
+        else:
+            monkeypatch.setenv("SLM_GATHER_STAGED", staged)
     loops = 7
     ta, tb = _targets(2, 256, False), _targets(2, 256, False)[::-1].copy()
     with lib.Plan(lib.ALGO_GS, 2, 256, 256, lib.TGT_F32, False, loops) as p:
@@ -197,12 +209,15 @@ def test_gather_overlaps_next_run_stream_ordered(gpu):
         for t in (ta, tb, ta):
             p.set_target(t)
             p.run(loops)
+            mode()
             p.gather_phase([2], 0)              # stage k, device only: no host sync
             buf = np.empty((2, 256, 256), np.float32)
             p.run(loops)                        # queued behind the staging copy, overlaps the transfer
+            mode()
             p.gather_phase([2], 0, buf)         # stage k ^ 1, then the host copy
             got.append(buf)
         p.mark(0)
+        mode()
         p.gather_phase([2], 0)
         p.mark(1)
         assert p.marked_ms() >= 0.0  # the stopwatch waits for the comm stream's gather

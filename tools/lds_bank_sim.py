@@ -61,7 +61,10 @@ def kernel_accesses(WV, PLOG, to_blocked, addr):
                     continue
                 yy, w = i // (RW // 4), (i % (RW // 4)) * 4
                 rm.append(addr(yy, w))
-                e = i * 4
+                j = i
+                if PW == 2:  # the kernel's `piece` lane order
+                    j = (i & ~63) | ((lane & 1) << 5) | (lane >> 1)
+                e = j * 4
                 q = e // (64 * PW)
                 rr = e - q * 64 * PW
                 by, bw = rr // PW, rr % PW
@@ -108,7 +111,7 @@ def main():
                 pad = [r for r in res if r[1].startswith("pad")][0]
                 shp = [r for r in res if r[1] == "shipped"][0]
                 print(f"WV={WV} P={1 << PLOG:2d} {'to_blocked  ' if tb else 'from_blocked'} "
-                      f"shipped {shp[0]:.2f}  r04 pad {pad[0]:.2f}  best {res[0][0]:.2f} ({res[0][1]})  "
+                      f"shipped {shp[0]:.2f}  padded rows {pad[0]:.2f}  best {res[0][0]:.2f} ({res[0][1]})  "
                       + ", ".join(f"{v:.2f} {n}" for v, n in res[1:4]))
 
 
