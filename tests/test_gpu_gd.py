@@ -106,6 +106,19 @@ def test_read_field_after_set_field(gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(1, 128, 256), (1, 90, 120)])  # radix plan, mixed-radix engine
+def test_read_field_without_state_is_an_error(gpu, shape):
+    """Before set_field and before any run a GD plan holds no field: reading
+    it is SLM_ERR_STATE on every engine, not the contents of a never-written
+    buffer."""
+    t = np.random.default_rng(3).uniform(0, 255, shape).astype(np.float32)
+    with gpu.Plan(gpu.ALGO_GD, *shape, gpu.TGT_F32, False, 3) as p:
+        p.set_target(t)
+        with pytest.raises(RuntimeError, match="no field yet"):
+            p.read_field()
+
+
+@pytest.mark.gpu
 def test_gd_fault_settled_before_gather(gpu):
     """A one-launch GD run whose grid wait gives up (SLM_GD_FAULT_TEST) is redone
     on the two-launch path before slm_plan_gather_phase / _stats ship its

@@ -161,3 +161,19 @@ def test_target_dtype_rules():
     for dt in (np.float64, np.float32, np.int32, np.uint16):
         t, tt = alg.target_for_device(np.zeros((64, 64), dt))
         assert tt == alg.TGT_F32 and t.dtype == np.float32
+
+
+def test_run_gs_multi_warns_when_exact_frames_stay_on_one_gpu(monkeypatch):
+    """float64 / wide-integer frames are not exact in float32, so run_gs_multi
+    keeps them on run_gs (one GPU, float64 error terms) and says that the
+    `devices` split is ignored; uint8 frames with one device do not warn."""
+    calls = []
+    monkeypatch.setattr(alg, "run_gs", lambda t, loops, tol, ain: calls.append(t.dtype) or "one-gpu")
+    t = np.random.default_rng(0).uniform(0, 255, (2, 8, 8))
+    with pytest.warns(RuntimeWarning, match="ignored"):
+        assert alg.run_gs_multi(t, 3, [0, 1]) == "one-gpu"
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        assert alg.run_gs_multi(t, 3, [0, 0]) == "one-gpu"  # one device: nothing is lost
+    assert calls == [np.float64, np.float64]
