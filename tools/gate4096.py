@@ -1,12 +1,14 @@
 #!/usr/bin/env python3
 """4096^2 warm-start precision survey over several targets and library builds.
 
-    python tools/gate4096.py --targets 0,1,2,3 [--libs default,<variant>...] [--spans 50,100] [--batch8]
+    python tools/gate4096.py --targets 0,1,2,3 [--libs default,<variant>...] [--plans default,wide]
+                             [--spans 50,100] [--batch8]
 
 For each bench target k (default_rng(1234 + k)) the float64
 oracle (oracle/fast_f64.py) runs 30 cold iterations, then `max(spans)` warm
 iterations with snapshots at every span; each library build (default = the
-in-tree libslm_hip.so, else lib/libslm_hip_<name>.so) then runs the same warm
+in-tree libslm_hip.so, else lib/libslm_hip_<name>.so) and each forced radix
+plan (--plans: $SLM_PLAN for the child, `default` = the library's pick) then runs the same warm
 starts on the GPU at float32 and float64 butterflies, in a child process per
 build, and the wrapped phase rms against the oracle is printed per (target,
 build, precision, span). --batch8 also runs the configs[4] per-GPU batch
@@ -101,6 +103,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--targets", default="0,1,2")
     ap.add_argument("--libs", default="default")
+    ap.add_argument("--plans", default="default")
     ap.add_argument("--spans", default="50,100")
     ap.add_argument("--batch8", action="store_true")
     ap.add_argument("--child", action="store_true")
@@ -117,10 +120,16 @@ def main():
     for name in args.libs.split(","):
         lib = os.path.join(ROOT, "spatial_light_modulator_module_amd", "lib",
                            "libslm_hip.so" if name == "default" else f"libslm_hip_{name}.so")
-        print(f"== build {name}", flush=True)
-        cmd = [sys.executable, os.path.abspath(__file__), "--child", "--tmp", tmp, "--name", name,
-               "--targets", args.targets, "--spans", args.spans] + (["--batch8"] if args.batch8 else [])
-        rc = max(rc, subprocess.call(cmd, env=dict(os.environ, SLM_LIB_PATH=lib)))
+        for plan in args.plans.split(","):
+            tag = name if plan == "default" else f"{name}_{plan}"
+            print(f"== build {name}, plan {plan}", flush=True)
+            cmd = [sys.executable, os.path.abspath(__file__), "--child", "--tmp", tmp, "--name", tag,
+                   "--targets", args.targets, "--spans", args.spans] + (["--batch8"] if args.batch8 else [])
+            env = dict(os.environ, SLM_LIB_PATH=lib)
+            env.pop("SLM_PLAN", None)
+            if plan != "default":
+                env["SLM_PLAN"] = plan
+            rc = max(rc, subprocess.call(cmd, env=env))
     return rc
 
 
