@@ -406,10 +406,11 @@ bool mr_big(int H, int W) {
 // per CU in a round) x e: so the rows per row tile / columns per column tile
 // minimise ceil(wgs / (cus occ)) * min(occ, ceil(wgs / cus)) * e (a grid one
 // workgroup too large for a round doubles the launch: 1080 rows in 540
-// two-row tiles on 512 slots did, 62.6 against ~35 us). Ties go to the
-// narrower column tile (more workgroups per CU: 1080 x 1920 columns of 2
-// measured 48.1 us against 54.5 us in tiles of 4, profiles/r05) and to the
-// wider row tile. $SLM_MR_RPW / $SLM_MR_CW override.
+// two-row tiles on 512 slots did, 62.6 against ~35 us). Column tiles that tie
+// go to 2 columns (32-B row segments), then the narrower: 1080 x 1920 columns
+// in tiles of 2 measured 48.2 us against 58.0 in tiles of 1 and 55.0 in tiles
+// of 4 (profiles/r05/mr_tiles_s13.txt); row tiles that tie go to the wider.
+// $SLM_MR_RPW / $SLM_MR_CW override.
 struct MrTiling {
     int rpw = 1, cw_log2 = 0;
 };
@@ -438,8 +439,8 @@ MrTiling mr_tiling(int B, int H, int W) {
         }
     }
     best = -1;
-    for (int c = 0; c <= 4; ++c) {
-        if (c > 0 && (((long long)H << c) > mr::kTileElems || (1 << c) > 2 * W)) break;
+    for (int c : {1, 0, 2, 3, 4}) {  // tie order
+        if (c > 0 && (((long long)H << c) > mr::kTileElems || (1 << c) > 2 * W)) continue;
         const int occ = mr::mr_col_occupancy(mr::CO_GS, big, ((size_t)H << c) * sizeof(double2));
         if (occ < 1) continue;
         const long long v = cost((long long)B * ((W + (1 << c) - 1) >> c), occ, (long long)H << c);

@@ -168,19 +168,48 @@ struct Lines {
     int count, ls, es;
 };
 
+// x / d for 0 <= x, x * d < 2^32 by one multiply-high (d > 1: mul = floor((2^32
+// - 1) / d) + 1, exact in that range; checked for every d <= 8192, x < 2^15):
+// the butterfly indexing divides by the pass's runtime span and line length
+// once per butterfly, which the compiler otherwise expands to a ~15-instruction
+// float-reciprocal sequence each
+struct FastDiv {
+    uint32_t d, mul;
+};
+__device__ __forceinline__ FastDiv fast_div(int d) {
+    return {(uint32_t)d, d > 1 ? 0xFFFFFFFFu / (uint32_t)d + 1u : 0u};
+}
+__device__ __forceinline__ int divq(int x, const FastDiv& f) {
+    return f.d == 1 ? x : (int)__umulhi((uint32_t)x, f.mul);
+}
+
 template <bool LINEFAST>
-__device__ __forceinline__ int bf_base(const Lines& g, int gi, int per_line, int L, int m, int& j) {
+__device__ __forceinline__ int bf_base(const Lines& g, int gi, const FastDiv& fpl, const FastDiv& fm,
+                                       const FastDiv& fc, int L, int& j) {
     int line, bf;
     if (LINEFAST) {
-        line = gi % g.count;
-        bf = gi / g.count;
+        bf = divq(gi, fc);
+        line = gi - bf * g.count;
     } else {
-        line = gi / per_line;
-        bf = gi - line * per_line;
+        line = divq(gi, fpl);
+        bf = gi - line * (int)fpl.d;
     }
-    const int blk = bf / m;
-    j = bf - blk * m;
+    const int blk = divq(bf, fm);
+    j = bf - blk * (int)fm.d;
     return line * g.ls + (blk * L + j) * g.es;
+}
+
+// twiddles w^q, q < R, of one butterfly from w = w_L^j: one table load, the
+// powers by complex products (float64: q ulp-scale errors, ~1e-15, where the
+// R - 1 table loads per butterfly were the passes' main vector-memory traffic)
+template <int R, bool INV>
+__device__ __forceinline__ void twiddle(double2 (&u)[R], double2 w1) {
+    double2 w = w1;
+#pragma unroll
+    for (int q = 1; q < R; ++q) {
+        if (q > 1) w = cmul(w, w1);
+        u[q] = INV ? cmulc(u[q], w) : cmul(u[q], w);
+    }
 }
 
 // one in-place pass of radix R and span L over every line of the tile
@@ -191,27 +220,17 @@ __device__ __forceinline__ void pass(double2* lds, const Lines& g, int n, int L,
     const int nb = g.count * per_line;
     const int tstride = n / L;
     const int step = m * g.es;
+    const FastDiv fpl = fast_div(per_line), fm = fast_div(m), fc = fast_div(g.count);
     for (int gi = threadIdx.x; gi < nb; gi += kThreads) {
         int j;
-        const int base = bf_base<LINEFAST>(g, gi, per_line, L, m, j);
+        const int base = bf_base<LINEFAST>(g, gi, fpl, fm, fc, L, j);
+        const double2 w1 = tw[j * tstride];
         double2 u[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) u[r] = lds[base + r * step];
-        if (DIT) {
-#pragma unroll
-            for (int q = 1; q < R; ++q) {
-                const double2 w = tw[q * j * tstride];
-                u[q] = INV ? cmulc(u[q], w) : cmul(u[q], w);
-            }
-        }
+        if (DIT) twiddle<R, INV>(u, w1);
         Dft<R, INV>::run(u);
-        if (!DIT) {
-#pragma unroll
-            for (int q = 1; q < R; ++q) {
-                const double2 w = tw[q * j * tstride];
-                u[q] = INV ? cmulc(u[q], w) : cmul(u[q], w);
-            }
-        }
+        if (!DIT) twiddle<R, INV>(u, w1);
 #pragma unroll
         for (int r = 0; r < R; ++r) lds[base + r * step] = u[r];
     }
