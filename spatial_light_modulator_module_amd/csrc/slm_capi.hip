@@ -1015,8 +1015,15 @@ int plan_create_on(int device, int algo, int batch, int height, int width, int t
     if (batch < 1 || max_loops < 1) return fail(SLM_ERR_ARG, "batch and max_loops must be >= 1");
     if (tgt_type != SLM_TGT_U8 && tgt_type != SLM_TGT_F32) return fail(SLM_ERR_ARG, "unknown target type");
     if (height < 1 || width < 1) return fail(SLM_ERR_ARG, "image shape %dx%d", height, width);
-    // sides without a radix plan (plans.hpp) run the DFT-GEMM engine (generic.hpp)
-    const bool generic = !slm_supported_length(height) || !slm_supported_length(width);
+    // sides without a radix plan (plans.hpp) run the any-size engine (generic.hpp:
+    // mixed-radix kernels, DFT-GEMM for large prime factors). $SLM_ENGINE=float64
+    // sends every shape there: complex128 state and float64 arithmetic
+    // throughout, the reference's own dtypes -- the radix plans keep complex64
+    // between their passes, which sets GD's float64-butterfly floor at ~3e-5
+    // rms after configs[2]'s 500 iterations (profiles/r05/gd_precision_s19.txt)
+    const char* eng = std::getenv("SLM_ENGINE");
+    const bool generic = (eng && !std::strcmp(eng, "float64")) || !slm_supported_length(height) ||
+                         !slm_supported_length(width);
     HIP_TRY(hipSetDevice(device));
     slm_plan* p = new slm_plan();
     p->algo = algo;

@@ -130,6 +130,36 @@ def test_gd_1024_configs2(gpu):
     assert rms < 2e-4
 
 
+@pytest.mark.gpu
+def test_gd_1024_configs2_at_500_float64_engine(gpu, monkeypatch):
+    """configs[2] at its own 500 iterations within the north-star 1e-5 rms:
+    $SLM_ENGINE=float64 runs the any-size engine (complex128 state, float64
+    arithmetic, numpy's dtype rules) on the radix-plan shape. The float32
+    plan's floor there is ~7e-5 (test_gd_1024_configs2) and float64
+    butterflies over the radix plans' complex64 passes ~3e-5."""
+    from spatial_light_modulator_module_amd import algorithms as alg
+
+    lib = gpu
+    n, loops = 1024, 500
+    t = bench_targets(0, 1, n)[0]
+    x0 = alg.make_initial_guess("random", None, t, 42)
+    monkeypatch.setenv("SLM_ENGINE", "float64")
+    with lib.Plan(lib.ALGO_GD, 1, n, n, lib.TGT_F32, False, loops) as p:
+        assert p.engine()[0] in ("mixed-radix", "dft-gemm"), p.engine()
+        p.set_target(t[None])
+        p.set_field(x0[None])
+        p.set_lr(np.full(loops, 0.005, np.float32))
+        p.run(loops, white_attention=1.0)
+        ph, _, stats, _ = p.read(expected=False)
+    ph_o, _, err_o, _ = fast_f64.gradient_descent_f64(t, loops, 0.005, 1.0,
+                                                      initial_field=x0.astype(np.complex64).astype(np.complex128))
+    rms = orc.phase_rms(ph[0], ph_o)
+    print(f"[parity] GD 1024^2 500 iterations, float64 engine: phase rms {rms:.3e}")
+    assert rms < PHASE_RMS_TOL
+    # (the plan takes the learning rates as float32: 0.005f is 2.2e-8 off the reference's 0.005)
+    np.testing.assert_allclose(stats[0, :loops, 3], err_o, rtol=1e-4)
+
+
 _ORACLE_4096 = {}
 
 
