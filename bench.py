@@ -309,6 +309,23 @@ def secondary(n, batch, iters, algo=_lib.ALGO_GS, precision=None, reps=3, width=
             "tiling": info}
 
 
+def north_star(extra):
+    """BASELINE.json north_star's bar (>= 60 % of the HBM roofline on the fused
+    GS loop at 4096 x 4096, evidenced by rocprof HBM bytes): each 4096^2 line's
+    iteration fraction on the PMC-counted bytes (profiles/pmc_traffic.json)
+    beside the bar, plus the sec-8(d) model and physical fractions."""
+    rows = {}
+    for key in ("gs_4096", "gs_4096_batch8"):
+        v = extra.get(key)
+        if isinstance(v, dict) and "iter_ms" in v:
+            rows[key] = {"iter_us_per_hologram": round(v["iter_ms_per_hologram"] * 1e3, 2),
+                         "iter_frac_of_hbm_peak_pmc": v.get("iter_frac_of_hbm_peak_pmc"),
+                         "iter_frac_of_hbm_peak_model": v.get("iter_frac_of_hbm_peak_model"),
+                         "iter_frac_of_hbm_peak_physical": v.get("iter_frac_of_hbm_peak_physical")}
+    return {"bar": 0.60, "basis": "iter_frac_of_hbm_peak_pmc (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE per launch "
+                                  "/ iteration time / 8 TB/s)", "shapes": rows}
+
+
 def main():
     opt = parse()
     if opt.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -480,6 +497,7 @@ def main():
         except _lib.SlmError as e:  # pragma: no cover - report, do not hide
             extra["error"] = str(e)
         out["extra"] = extra
+        out["north_star"] = north_star(extra)
     if world == 1 and not opt.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, iters, opt.cpu_sample_seconds)
         out["cpu_baseline_all_cores"] = cpu_baseline_all_cores(n, iters, opt.cpu_sample_seconds / 2)

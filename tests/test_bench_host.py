@@ -192,3 +192,19 @@ def test_cpu_baseline_configs0_times_whole_runs():
     assert cb["unit"] == "holograms/s" and cb["cores"] == 1 and cb["kind"] == "port"
     assert cb["value"] > 0 and abs(cb["value"] * cb["s_per_hologram"] - 1) < 1e-9
     assert cb["host_cpus"] == os.cpu_count() and "configs[0]" in cb["sample"]
+
+
+def test_north_star_summary_reports_the_pmc_fraction_per_4096_line():
+    """The bench line's north_star block carries each 4096^2 extra line's
+    PMC-based iteration fraction beside BASELINE.json's 60 % bar."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    line = {"iter_ms": 1.17, "iter_ms_per_hologram": 0.1467, "iter_frac_of_hbm_peak_pmc": 0.53,
+            "iter_frac_of_hbm_peak_model": 0.97, "iter_frac_of_hbm_peak_physical": 0.51}
+    ns = bench.north_star({"gs_4096_batch8": line, "gd_1024": {"iter_ms": 0.02}, "error": "x"})
+    assert ns["bar"] == 0.60 and "pmc" in ns["basis"]
+    assert list(ns["shapes"]) == ["gs_4096_batch8"]
+    assert ns["shapes"]["gs_4096_batch8"] == {"iter_us_per_hologram": 146.7, "iter_frac_of_hbm_peak_pmc": 0.53,
+                                              "iter_frac_of_hbm_peak_model": 0.97,
+                                              "iter_frac_of_hbm_peak_physical": 0.51}
