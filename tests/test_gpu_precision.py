@@ -80,3 +80,24 @@ def test_warm_start_parity_large(gpu, n, span, u8, seed):
               f"phase rms {rms:.3e}")
         assert rms < PHASE_RMS_TOL
         np.testing.assert_allclose(err, ref_err, rtol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1234, 1235])
+def test_headline_on_the_float64_engine(gpu, monkeypatch, seed):
+    """The headline configuration (GS 1024^2, +200 from the oracle's 30-iteration
+    state, the bench's own targets) on $SLM_ENGINE=float64 -- complex128 state
+    and float64 arithmetic, as the reference -- lands orders of magnitude
+    inside the 1e-5 bar that the float32 plans meet with ~2x margin."""
+    t = np.random.default_rng(seed).uniform(0, 255, (1024, 1024)).astype(np.float32)
+    with sfft.set_workers(WORKERS):
+        phi_w, _, _ = orc.gerchberg_saxton_faithful(t, 30)
+        ref, _, ref_err = orc.gerchberg_saxton_faithful(t, 200, initial_phase=phi_w)
+    monkeypatch.setenv("SLM_ENGINE", "float64")
+    with gpu.Plan(gpu.ALGO_GS, 1, 1024, 1024, gpu.TGT_F32, False, 200) as p:
+        assert p.engine()[0] == "mixed-radix", p.engine()
+    ph, err = _gpu_warm_run(gpu, t, phi_w, 200, gpu.PRECISION_F64)
+    rms = orc.phase_rms(ph, ref)
+    print(f"[parity] 1024^2 f32 target (seed {seed}), float64 engine: warm-start 30+200: phase rms {rms:.3e}")
+    assert rms < 1e-6
+    np.testing.assert_allclose(err, ref_err, rtol=1e-5)
