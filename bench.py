@@ -257,13 +257,26 @@ def _round(v):
     return round(v, 4) if isinstance(v, float) else v
 
 
-def secondary(n, batch, iters, algo=_lib.ALGO_GS, precision=None, reps=3, width=None):
+def secondary(n, batch, iters, algo=_lib.ALGO_GS, precision=None, reps=3, width=None, engine=None):
     """Extra single-GPU measurements: one-run wall time and the per-kernel
     roofline of another configuration (4096^2 HBM stress, batched 1024^2, GD,
-    float64 butterflies, an n x width SLM panel on the any-size engine)."""
+    float64 butterflies, an n x width SLM panel on the any-size engine).
+    engine="float64": the plan is created under $SLM_ENGINE=float64 (complex128
+    state and arithmetic: the complex128 radix-plan kernels on these sides)."""
     w = width or n
     t = targets(0, batch, n, w)
-    with _lib.Plan(algo, batch, n, w, _lib.TGT_F32, False, iters) as plan:
+    saved = os.environ.get("SLM_ENGINE")
+    if engine:
+        os.environ["SLM_ENGINE"] = engine
+    try:
+        plan = _lib.Plan(algo, batch, n, w, _lib.TGT_F32, False, iters)
+    finally:
+        if engine:
+            if saved is None:
+                os.environ.pop("SLM_ENGINE", None)
+            else:
+                os.environ["SLM_ENGINE"] = saved
+    with plan:
         plan.set_target(t)
         if precision is not None:
             plan.set_precision(precision)
@@ -288,16 +301,19 @@ def secondary(n, batch, iters, algo=_lib.ALGO_GS, precision=None, reps=3, width=
     # bytes the launches of one iteration physically move (slm_plan_kernel_bytes)
     phys_iter = sum(r["physical_bytes_per_launch"] for r in rows.values())
     name = "gd" if algo == _lib.ALGO_GD else "gs"
-    traffic = pmc_traffic(f"{name}_{n}x{w}_b{batch}_it{iters}_{info['precision']}")  # rocprofv3 PMC, profiles/
+    # rocprofv3 PMC, profiles/ (keyed by engine too: complex128 plans move other bytes)
+    eng_tag = "" if plan_engine[0] in ("stockham", "shuffle") else "_" + plan_engine[0]
+    traffic = pmc_traffic(f"{name}_{n}x{w}_b{batch}_it{iters}_{info['precision']}{eng_tag}")
     for k, row in rows.items():
         row["traffic_bytes_per_launch"] = None if traffic is None else traffic.get(k)
     per_px = 76 if algo == _lib.ALGO_GD else 68
     # the north-star fraction on bytes moved: the committed rocprofv3 PMC traffic
     # (FETCH_SIZE x 2 + WRITE_SIZE per launch, profiles/pmc_traffic.json) of one
-    # column and one row launch -- a GS iteration -- over the measured iteration time
+    # iteration's launches (GS: a column and a row launch; GD: the column
+    # launches and the row launch) over the measured iteration time
     pmc_frac = None
-    if traffic and algo == _lib.ALGO_GS and traffic.get("col_main") and traffic.get("row_main"):
-        pmc_frac = round((traffic["col_main"] + traffic["row_main"]) / iter_s / 1e9 / HBM_PEAK_GBS, 4)
+    if traffic and all(traffic.get(k) for k in rows):
+        pmc_frac = round(sum(traffic[k] for k in rows) / iter_s / 1e9 / HBM_PEAK_GBS, 4)
     return {"algo": name, "shape": [batch, n, w], "iters": iters, "engine": list(plan_engine),
             "iter_frac_of_hbm_peak_pmc": pmc_frac,
             "holograms_per_s": batch / wall, "iter_ms": iter_s * 1e3, "iter_ms_per_hologram": iter_s * 1e3 / batch,
@@ -307,6 +323,58 @@ def secondary(n, batch, iters, algo=_lib.ALGO_GS, precision=None, reps=3, width=
             "dominant_frac_of_hbm_peak_model": round(rows[dom]["achieved_gbs"] / HBM_PEAK_GBS, 4),
             "dominant_frac_of_hbm_peak_physical": round(rows[dom]["physical_gbs"] / HBM_PEAK_GBS, 4),
             "tiling": info}
+
+
+def summary(out):
+    """The bench line's last object: every measured configuration in a few
+    numbers (the driver keeps only the tail of a long line). Per line: us per
+    hologram-iteration, holograms/s, the iteration's fraction of 8 TB/s on
+    PMC-counted bytes (profiles/pmc_traffic.json) and on the bytes the kernels
+    move, and the engine."""
+    s = {"value": out["value"], "unit": out["unit"], "gs_iter_us": round(out["gs_iter_ms"] * 1e3, 3),
+         "roofline_frac": out["roofline"]["frac"], "roofline_frac_physical": out["roofline"]["frac_physical"],
+         "dominant": out["roofline"]["kernel"]}
+    lines = {}
+    for k, v in out.get("extra", {}).items():
+        if isinstance(v, dict) and "iter_ms" in v:
+            lines[k] = [round(v["iter_ms_per_hologram"] * 1e3, 2), round(v["holograms_per_s"], 2),
+                        v.get("iter_frac_of_hbm_peak_pmc"), v.get("iter_frac_of_hbm_peak_physical"),
+                        v["engine"][0]]
+    if lines:
+        s["lines"] = {"columns": ["us_per_hologram_iter", "holograms_per_s", "frac_pmc", "frac_physical", "engine"],
+                      **lines}
+    pc = out.get("extra", {}).get("pcie_inclusive")
+    if pc:
+        s["pcie_inclusive_holograms_per_s"] = round(pc["holograms_per_s"], 2)
+    for k in ("cpu_baseline", "cpu_baseline_all_cores", "cpu_baseline_configs0"):
+        if k in out:
+            s[k] = round(out[k]["value"], 4)
+    if "parity" in out:
+        s["parity"] = out["parity"]
+    return s
+
+
+def headline_parity(n, iters):
+    """SURVEY.md 8c warm-start parity of the timed configuration, measured in
+    this run: bench target 0 (the first hologram of every step), the float64
+    restatement's phase after 30 cold iterations, `iters` more on the bench's
+    plan configuration vs `iters` more of the restatement (oracle/fast_f64.py,
+    threaded pocketfft; pinned to the reference goldens by the CPU tests).
+    North-star bar 1e-5 rms."""
+    from oracle import fast_f64
+    from oracle import gs_gd_oracle as orc
+
+    t = targets(0, 1, n)[0]
+    t0 = time.perf_counter()
+    phi30 = fast_f64.gerchberg_saxton_f64(t, 30)[0].astype(np.float32)
+    ref = fast_f64.gerchberg_saxton_f64(t, iters, initial_phase=phi30)[0]
+    with _lib.Plan(_lib.ALGO_GS, 1, n, n, _lib.TGT_F32, False, iters) as p:
+        p.set_target(t[None])
+        p.set_phase(phi30[None])
+        p.run(iters)
+        ph = p.read(expected=False, stats=False, iters=False)[0][0]
+    return {"gs_warm30_plus_iters_phase_rms": float(f"{orc.phase_rms(ph, ref):.3e}"), "bar": 1e-5,
+            "target": "bench target 0", "oracle_s": round(time.perf_counter() - t0, 1)}
 
 
 def north_star(extra):
@@ -494,14 +562,23 @@ def main():
             f64 = _lib.PRECISION_F64  # float64 butterflies (parity margin)
             extra["f64_gs_1024"] = secondary(1024, 1, 200, precision=f64)
             extra["f64_gs_4096"] = secondary(4096, 1, 200, precision=f64)
+            # complex128 state and arithmetic ($SLM_ENGINE=float64: the reference's own
+            # dtypes on the radix-plan kernels), configs[4]'s and configs[2]'s run lengths
+            extra["c128_gs_4096"] = secondary(4096, 1, 200, engine="float64", reps=2)
+            extra["c128_gd_1024"] = secondary(1024, 1, 500, algo=_lib.ALGO_GD, engine="float64", reps=2)
         except _lib.SlmError as e:  # pragma: no cover - report, do not hide
             extra["error"] = str(e)
         out["extra"] = extra
         out["north_star"] = north_star(extra)
+        try:
+            out["parity"] = headline_parity(n, iters)
+        except _lib.SlmError as e:  # pragma: no cover - report, do not hide
+            out["parity"] = {"error": str(e)}
     if world == 1 and not opt.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(n, iters, opt.cpu_sample_seconds)
         out["cpu_baseline_all_cores"] = cpu_baseline_all_cores(n, iters, opt.cpu_sample_seconds / 2)
         out["cpu_baseline_configs0"] = cpu_baseline_configs0()
+    out["summary"] = summary(out)  # last: inside the driver's tail of the line
     print(json.dumps(out), flush=True)
     plan.close()
     if world > 1:

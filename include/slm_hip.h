@@ -141,9 +141,12 @@ int slm_plan_layout(slm_plan* plan, int* x_log2, int* y_log2);
 /* transform engine of the GS iteration kernels: 0 = Stockham pair (LDS
  * exchange before every pass), 1 = wave-shuffle pair (fft_shuffle.hpp: 1024-
  * point lines, float32; v_permlane swaps for four of the six exchanges; the
- * GS and GD iteration kernels), 2 = DFT-GEMM (float64 DFT matrices on rocBLAS
- * ZGEMM: sides with a prime factor above 13), 3 = mixed radix (float64
- * in-place radix-2..13 kernels: other sides without a float32 radix plan) */
+ * GS and GD iteration kernels), 2 = line transforms (float64 1-D transforms
+ * along rows and transposed columns, Bluestein's chirp-z for a side with a
+ * prime factor above 13), 3 = mixed radix (float64 in-place radix-2..13
+ * kernels: other sides without a float32 radix plan), 4 = complex128 radix
+ * plans (float64 Stockham kernels with complex128 state: 2^k / 768 sides
+ * under $SLM_ENGINE=float64) */
 int slm_plan_engine(slm_plan* plan, int* col_engine, int* row_engine);
 /* HIP device the plan lives on */
 int slm_plan_device(slm_plan* plan);
@@ -184,7 +187,7 @@ int slm_gs_multi_timing(int max_shards, double* wall_ms, double* run_ms);
 int slm_fft2(const float* in_re_im, float* out_re_im, int batch, int height, int width, int inverse);
 /* unscaled 2-D C2C transform of [batch][h][w] complex128 in float64 arithmetic
  * (any shape: mixed-radix kernels where both sides factor into 2..13, else
- * DFT-GEMM) -> the float64 scipy.fft.ifft2 of move_traps.update_hologram,
+ * chirp-z line transforms) -> the float64 scipy.fft.ifft2 of move_traps.update_hologram,
  * src/move_traps.py:66 (times h w) */
 int slm_fft2_c128(const double* in_re_im, double* out_re_im, int batch, int height, int width, int inverse);
 

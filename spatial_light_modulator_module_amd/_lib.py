@@ -347,11 +347,14 @@ class Plan:
         """(column, row) transform engine of the GS iteration kernels:
         "stockham", "shuffle" (wave-shuffle pair, fft_shuffle.hpp) or, for
         sides without a float32 radix plan, "mixed-radix" (float64 radix
-        2..13 kernels, mixed_radix.hpp) or "dft-gemm" (float64 DFT matrices
-        on rocBLAS ZGEMM, generic.hip: sides with a larger prime factor)."""
+        2..13 kernels, mixed_radix.hpp) or "bluestein" (float64 1-D line
+        transforms along rows and transposed columns, Bluestein's chirp-z
+        for a side with a larger prime factor, generic.hip), and under
+        $SLM_ENGINE=float64 on 2^k / 768 sides "radix-c128" (float64
+        Stockham kernels with complex128 state, radix_c128.hpp)."""
         c, r = ctypes.c_int(), ctypes.c_int()
         check(self._lib.slm_plan_engine(self.handle, ctypes.byref(c), ctypes.byref(r)), "slm_plan_engine")
-        names = ("stockham", "shuffle", "dft-gemm", "mixed-radix")
+        names = ("stockham", "shuffle", "bluestein", "mixed-radix", "radix-c128")
         return names[c.value], names[r.value]
 
     def layout(self) -> tuple[int, int]:

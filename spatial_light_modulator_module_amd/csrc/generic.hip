@@ -1,34 +1,31 @@
 // Any-size engine (generic.hpp): GS / GD iterations on image sides that no
 // float32 radix plan covers, in complex float64 like the reference's loop.
 //
-// Two transform back ends:
+// Three transform back ends:
+//  * complex128 radix plans (radix_c128.hpp; the default where both sides
+//    have a radix plan, plans.hpp: 2^k and 768 -- reached through
+//    $SLM_ENGINE=float64): the mixed-radix launch structure and contract on
+//    compile-time Stockham transforms with the line in registers and
+//    complex128 LDS exchanges;
 //  * mixed radix (mixed_radix.hpp, mr_inst.hip; the default wherever both
 //    sides factor into 2, 3, 5, 7, 11, 13 and fit a workgroup's LDS): the
 //    iteration is two fused launches -- column pass (forward transform,
 //    projection and statistics, inverse transform) and row pass (inverse,
 //    projection, forward) -- O(N log N), hand-written kernels only;
-//  * DFT-GEMM (any other side, e.g. one with a large prime factor, or
-//    $SLM_GENERIC_ENGINE=gemm): the 2-D transforms as products with the
-//    dense DFT matrices on rocBLAS ZGEMM, O(N^3), with element-wise kernels.
-//
-// DFT-GEMM: row-major [H][W] images are, to a column-major BLAS, W x H
-// matrices M^T (leading dimension W). With the symmetric DFT matrices
-// F_N[j][k] = exp(-2 pi i jk / N):
-//     fft2(M) = F_H M F_W   <=>   fft2(M)^T = F_W M^T F_H
-// so a forward 2-D transform is T = F_W M^T (m = W, n = H, k = W), then
-// T F_H (m = W, n = H, k = H); the inverse (unscaled) takes the conjugate
-// transposes, which are the conjugates: op = rocblas_operation_conjugate_transpose.
-// Every hologram of the batch shares the matrices (stride 0 in the batched
-// product). ZGEMM runs with atomics disabled, so a product of the same
-// operands is the same bits every time (a stopped hologram of a checked run is
-// frozen by leaving its inputs untouched, see enqueue).
+//  * line transforms (any other side, e.g. one with a large prime factor, or
+//    $SLM_GENERIC_ENGINE=bluestein): each 2-D transform is a pass of 1-D
+//    transforms along the rows, a tiled transpose, a pass along the (former)
+//    columns and a transpose back, with element-wise kernels between the
+//    transforms. A side with a mixed-radix plan transforms directly; any other
+//    side by Bluestein's chirp-z over a mixed-radix length M >= 2n - 1
+//    (mr_line_kernel, mr_inst.hip) -- O(N log N) for every length, hand-written
+//    kernels only. (Until r05 these sides were products with dense DFT matrices
+//    on rocBLAS ZGEMM, O(N^3).)
 //
 // Numerics follow the reference's float64 path (src/algorithms.py:10-49,
 // 60-112): complex128 state, float64 statistics (E = |C|^2 unrounded),
 // amplitudes as numpy forms them (sqrt(uint8) -> float16, sqrt(float32) ->
 // float32), the cold start's ifft2 of a float amplitude rounded to complex64.
-#include <rocblas/rocblas.h>
-
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -39,6 +36,7 @@
 #include "generic.hpp"
 #include "kernels.hpp"
 #include "mixed_radix.hpp"
+#include "radix_c128.hpp"
 
 int slm_set_error(int code, const char* msg);  // slm_capi.hip
 
@@ -47,6 +45,11 @@ namespace slm {
 struct GenericEngine {
     // mixed-radix back end: line plans (twiddles, digit reversal) of both sides
     bool mr = false;
+    // complex128 radix-plan back end (mr is set too: same launch structure and
+    // buffers; its line plans hold Stockham twiddle tables and the identity order)
+    bool rz = false;
+    int rkey = -1, ckey = -1;  // plan keys (plans.hpp) of the row / column transforms
+    int rz_cw = 0;             // columns per column tile
     bool big = false;        // a radix outside mr::small_radix in either plan (7, 11, 13)
     mr::LinePlan pw, ph;     // row (length W) and column (length H) transforms
     int rpw = 1;             // rows per row tile
@@ -54,16 +57,16 @@ struct GenericEngine {
     int nwg_col = 0;         // column tiles per hologram
     std::vector<void*> tables;  // device twiddle / reversal tables
     float* ain_rev = nullptr;   // a_in with rows in the row transform's digit-reversed order (has_ain)
-    // DFT-GEMM back end
-    rocblas_handle blas = nullptr;
-    double2* fh = nullptr;   // F_H [H][H]
-    double2* fw = nullptr;   // F_W [W][W] (== fh for square images)
+    // line-transform back end: the row (length W) and column (length H) transforms
+    mr::LineArgs lw, lh;
+    bool big_w = false, big_h = false;  // their plans need the odd-radix kernels
     // state (row-major complex128 [B][H][W])
-    double2* a = nullptr;    // GEMM GS: A; GD: the inverse-transformed gradient g. Mixed radix: row-pass output
-    double2* b = nullptr;    // GEMM GS: B, then C in place; GD: u, then F in place. Mixed radix: column-pass output
-    double2* d = nullptr;    // GEMM GS: D; GD: G
+    double2* a = nullptr;    // lines GS: A; GD: the inverse-transformed gradient g. Mixed radix: row-pass output
+    double2* b = nullptr;    // lines GS: B, then C in place; GD: u, then F in place. Mixed radix: column-pass output
+    double2* d = nullptr;    // lines GS: D; GD: G
     double2* x = nullptr;    // GD: the field x
-    double2* tmp = nullptr;  // GEMM product intermediate
+    double2* tmp = nullptr;  // lines: the row-transformed image
+    double2* tmp2 = nullptr; // lines: the transposed image [B][W][H]
 };
 
 namespace {
@@ -74,11 +77,6 @@ constexpr int kGT = 256;  // threads per block of the element-wise kernels
     do {                                                                                 \
         hipError_t e_ = (expr);                                                          \
         if (e_ != hipSuccess) return slm_set_error(SLM_ERR_HIP, hipGetErrorString(e_));  \
-    } while (0)
-#define G_BLAS(expr)                                                                     \
-    do {                                                                                 \
-        rocblas_status s_ = (expr);                                                      \
-        if (s_ != rocblas_status_success) return slm_set_error(SLM_ERR_HIP, rocblas_status_to_string(s_)); \
     } while (0)
 
 int grid_of(long long n) { return (int)std::min<long long>(16384, (n + kGT - 1) / kGT); }
@@ -309,28 +307,48 @@ __global__ void __launch_bounds__(kGT) k_gd_update(double2* X, const double2* g,
     }
 }
 
-std::vector<double> dft_matrix(int n) {
-    std::vector<double> m((size_t)n * n * 2);
-    for (long long j = 0; j < n; ++j)
-        for (long long k = 0; k < n; ++k) {
-            const double ang = -2.0 * M_PI * (double)((j * k) % n) / (double)n;
-            m[(j * n + k) * 2] = std::cos(ang);
-            m[(j * n + k) * 2 + 1] = std::sin(ang);
-        }
-    return m;
+// [B][R][C] -> [B][C][R] complex128 through 32 x 32 LDS tiles (the line
+// transforms run along contiguous rows only)
+__global__ void __launch_bounds__(256) k_transpose(const double2* in, double2* out, int R, int C) {
+    __shared__ double2 tile[32][33];
+    const long long hb = (long long)blockIdx.z * R * C;
+    const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    for (int k = ty; k < 32; k += 8) {
+        const int r = r0 + k, c = c0 + tx;
+        if (r < R && c < C) tile[k][tx] = in[hb + (long long)r * C + c];
+    }
+    __syncthreads();
+    for (int k = ty; k < 32; k += 8) {
+        const int c = c0 + k, r = r0 + tx;
+        if (r < R && c < C) out[hb + (long long)c * R + r] = tile[tx][k];
+    }
 }
 
-// out = op2(in): forward (F) or inverse (conj F, unscaled) 2-D transform of
-// [B][H][W] complex128; in may equal out (the product goes through tmp)
+// 1-D transforms of `lines` rows of the line plan's length
+int line_pass(const GenericEngine* g, const mr::LineArgs& base, bool big, const double2* in, double2* out,
+              long long lines, bool inverse, hipStream_t st) {
+    if (lines > 0x7fffffffLL) return slm_set_error(SLM_ERR_UNSUPPORTED, "line transforms: too many lines");
+    mr::LineArgs a = base;
+    a.in = in;
+    a.out = out;
+    a.inverse = inverse ? 1 : 0;
+    if (mr::mr_line_launch(big, a, (int)lines, (size_t)a.pl.n * sizeof(double2), st))
+        return slm_set_error(SLM_ERR_HIP, "line transform launch failed");
+    return 0;
+}
+
+// out = op(in): forward or inverse (unscaled) 2-D transform of [B][H][W]
+// complex128 as rows -> transpose -> rows -> transpose; in may equal out
 int dft2(GenericEngine* g, const GenericView& v, const double2* in, double2* out, bool inverse) {
-    const rocblas_operation opf = inverse ? rocblas_operation_conjugate_transpose : rocblas_operation_none;
-    const rocblas_double_complex one{1.0, 0.0}, zero{0.0, 0.0};
-    auto cz = [](const double2* p) { return reinterpret_cast<const rocblas_double_complex*>(p); };
-    auto z = [](double2* p) { return reinterpret_cast<rocblas_double_complex*>(p); };
-    G_BLAS(rocblas_zgemm_strided_batched(g->blas, opf, rocblas_operation_none, v.W, v.H, v.W, &one, cz(g->fw), v.W, 0,
-                                         cz(in), v.W, v.holo, &zero, z(g->tmp), v.W, v.holo, v.B));
-    G_BLAS(rocblas_zgemm_strided_batched(g->blas, rocblas_operation_none, opf, v.W, v.H, v.H, &one, cz(g->tmp), v.W,
-                                         v.holo, cz(g->fh), v.H, 0, &zero, z(out), v.W, v.holo, v.B));
+    hipStream_t st = v.stream;
+    if (int rc = line_pass(g, g->lw, g->big_w, in, g->tmp, (long long)v.B * v.H, inverse, st)) return rc;
+    hipLaunchKernelGGL(k_transpose, dim3((v.W + 31) / 32, (v.H + 31) / 32, v.B), dim3(256), 0, st, g->tmp, g->tmp2,
+                       v.H, v.W);
+    if (int rc = line_pass(g, g->lh, g->big_h, g->tmp2, g->tmp2, (long long)v.B * v.W, inverse, st)) return rc;
+    hipLaunchKernelGGL(k_transpose, dim3((v.H + 31) / 32, (v.W + 31) / 32, v.B), dim3(256), 0, st, g->tmp2, out,
+                       v.W, v.H);
+    G_HIP(hipGetLastError());
     return 0;
 }
 
@@ -382,14 +400,16 @@ bool mr_radices(int n, std::vector<int>& rad) {
     return t == 1 && (int)rad.size() <= mr::kMaxPass;
 }
 
-bool mr_forced_gemm() {
+// $SLM_GENERIC_ENGINE=bluestein (alias: gemm, r05's name of that back end)
+// sends every side through the line transforms, chirp-z included
+bool mr_forced_lines() {
     const char* e = std::getenv("SLM_GENERIC_ENGINE");
-    return e && !std::strcmp(e, "gemm");
+    return e && (!std::strcmp(e, "bluestein") || !std::strcmp(e, "gemm"));
 }
 
 bool mr_shape_ok(int H, int W) {
     std::vector<int> r;
-    return !mr_forced_gemm() && mr_radices(H, r) && mr_radices(W, r);
+    return !mr_forced_lines() && mr_radices(H, r) && mr_radices(W, r);
 }
 
 bool mr_big(int H, int W) {
@@ -459,7 +479,7 @@ MrTiling mr_tiling(int B, int H, int W) {
 }
 
 // twiddles exp(-2 pi i t / n) and the DIF output order's natural indices
-int mr_plan_line(GenericEngine* g, int n, mr::LinePlan* pl, hipStream_t st) {
+int mr_plan_line(GenericEngine* g, int n, mr::LinePlan* pl, hipStream_t st, std::vector<int>* rev_out = nullptr) {
     std::vector<int> rad;
     if (!mr_radices(n, rad)) return slm_set_error(SLM_ERR_UNSUPPORTED, "mixed radix: unsupported length");
     pl->n = n;
@@ -493,6 +513,94 @@ int mr_plan_line(GenericEngine* g, int n, mr::LinePlan* pl, hipStream_t st) {
     G_HIP(hipStreamSynchronize(st));
     pl->tw = static_cast<const double2*>(dtw);
     pl->rev = static_cast<const int*>(drev);
+    if (rev_out) *rev_out = rev;
+    return 0;
+}
+
+bool plan_big(int n) {
+    std::vector<int> r;
+    if (!mr_radices(n, r)) return false;
+    for (int x : r)
+        if (!mr::small_radix(x)) return true;
+    return false;
+}
+
+// Line transform of length n (mr::LineArgs): direct where n has a mixed-radix
+// plan (unless `chirp_z`), else Bluestein over the smallest M >= 2n - 1 made of
+// the radices 2, 3, 4, 5, 8 (the small-radix kernels): the chirp w_j =
+// exp(i pi j^2 / n) (angle from j^2 mod 2n, exact) and bhat = FFT_M(b) / M in
+// the DIF output order, b_m = w_m for m < n, b_(M - m) = w_m for 0 < m < n,
+// else 0 (one O(M^2) float64 DFT at plan creation, from a table of the M roots)
+int line_plan(GenericEngine* g, int n, bool chirp_z, mr::LineArgs* la, bool* big, hipStream_t st) {
+    std::vector<int> rad;
+    *la = mr::LineArgs{};
+    la->n = n;
+    if (!chirp_z && mr_radices(n, rad)) {
+        la->direct = 1;
+        *big = plan_big(n);
+        return mr_plan_line(g, n, &la->pl, st);
+    }
+    int M = std::max(1, 2 * n - 1);
+    auto smooth5 = [](int m) {
+        for (int p : {2, 3, 5})
+            while (m % p == 0) m /= p;
+        return m == 1;
+    };
+    while (!smooth5(M)) ++M;
+    if (M > mr::kMaxLine)
+        return slm_set_error(SLM_ERR_UNSUPPORTED, "line transforms: side too long for one workgroup's chirp-z line");
+    std::vector<int> rev;
+    if (int rc = mr_plan_line(g, M, &la->pl, st, &rev)) return rc;
+    la->direct = 0;
+    *big = plan_big(M);
+    std::vector<double> chirp((size_t)n * 2), b((size_t)M * 2, 0.0), bh((size_t)M * 2);
+    for (long long j = 0; j < n; ++j) {
+        const double ang = M_PI * (double)((j * j) % (2LL * n)) / (double)n;
+        chirp[j * 2] = std::cos(ang);
+        chirp[j * 2 + 1] = std::sin(ang);
+        b[j * 2] = chirp[j * 2];
+        b[j * 2 + 1] = chirp[j * 2 + 1];
+        if (j > 0) {
+            b[(M - j) * 2] = chirp[j * 2];
+            b[(M - j) * 2 + 1] = chirp[j * 2 + 1];
+        }
+    }
+    std::vector<double> rc_((size_t)M), rs_((size_t)M);
+    for (int t = 0; t < M; ++t) {
+        const double ang = 2.0 * M_PI * (double)t / (double)M;
+        rc_[t] = std::cos(ang);
+        rs_[t] = -std::sin(ang);
+    }
+    std::vector<double> bhat((size_t)M * 2);
+    for (long long k = 0; k < M; ++k) {
+        double re = 0.0, im = 0.0;
+        long long idx = 0;
+        for (long long m = 0; m < M; ++m) {
+            const double br = b[m * 2], bi = b[m * 2 + 1];
+            if (br != 0.0 || bi != 0.0) {
+                re += br * rc_[idx] - bi * rs_[idx];
+                im += br * rs_[idx] + bi * rc_[idx];
+            }
+            idx += k;
+            if (idx >= M) idx -= M;
+        }
+        bhat[k * 2] = re / M;
+        bhat[k * 2 + 1] = im / M;
+    }
+    for (int e = 0; e < M; ++e) {
+        bh[(size_t)e * 2] = bhat[(size_t)rev[e] * 2];
+        bh[(size_t)e * 2 + 1] = bhat[(size_t)rev[e] * 2 + 1];
+    }
+    void *dc = nullptr, *db = nullptr;
+    if (hipMalloc(&dc, chirp.size() * sizeof(double)) != hipSuccess) return slm_set_error(SLM_ERR_HIP, "line transforms: allocation");
+    g->tables.push_back(dc);
+    if (hipMalloc(&db, bh.size() * sizeof(double)) != hipSuccess) return slm_set_error(SLM_ERR_HIP, "line transforms: allocation");
+    g->tables.push_back(db);
+    G_HIP(hipMemcpyAsync(dc, chirp.data(), chirp.size() * sizeof(double), hipMemcpyHostToDevice, st));
+    G_HIP(hipMemcpyAsync(db, bh.data(), bh.size() * sizeof(double), hipMemcpyHostToDevice, st));
+    G_HIP(hipStreamSynchronize(st));
+    la->chirp = static_cast<const double2*>(dc);
+    la->bhat = static_cast<const double2*>(db);
     return 0;
 }
 
@@ -504,6 +612,96 @@ int mr_roots(hipStream_t st) {
             roots[R * mr::kMaxRadix + q] = make_double2(std::cos(ang), -std::sin(ang));
         }
     if (mr::mr_set_roots(roots.data(), st)) return slm_set_error(SLM_ERR_HIP, "mixed radix: root table upload failed");
+    return 0;
+}
+
+// ------------------------------------------------------------------------
+// complex128 radix-plan back end (host side)
+// ------------------------------------------------------------------------
+// Plan key of one axis: both sides need a built radix plan (rz::key_built).
+// As the float32 engine's pick: the narrow variant (half the elements per
+// thread) where the wide one would leave fewer than 4 waves per SIMD over
+// the chip, else the wide one; $SLM_RZ_PLAN=wide|narrow forces a variant.
+int rz_key(int n, long long elems) {
+    const int wide = plan_index(n, 0), narrow = plan_index(n, 1);
+    const bool w_ok = rz::key_built(wide), n_ok = rz::key_built(narrow);
+    if (!w_ok && !n_ok) return -1;
+    if (!w_ok) return narrow;
+    if (!n_ok) return wide;
+    if (const char* s = std::getenv("SLM_RZ_PLAN")) {
+        if (!std::strcmp(s, "wide")) return wide;
+        if (!std::strcmp(s, "narrow")) return narrow;
+    }
+    const long long waves = elems / kPlans[wide].e / 64;
+    return waves < 4LL * 1024 ? narrow : wide;
+}
+
+// Columns per column tile: 256 threads where the line's LDS allows two
+// workgroups per CU (4 columns of 64 threads, 2 of 128), 2 for 256-thread
+// lines (4096: one 512-thread workgroup per CU, 32-B row segments), 8 for
+// 8-thread lines; $SLM_RZ_CW overrides.
+int rz_cw_of(int ckey, int W) {
+    const int T = kPlans[ckey].n / kPlans[ckey].e;
+    int cw = T >= 128 ? 2 : T >= 16 ? 4 : 8;
+    if (const char* e = std::getenv("SLM_RZ_CW")) cw = std::atoi(e);
+    if (cw < 1 || W % cw || !rz::rz_col_ok(ckey, cw)) return 0;
+    return cw;
+}
+
+struct RzChoice {
+    int rkey = -1, ckey = -1, cw = 0;
+};
+bool rz_shape(int B, int H, int W, RzChoice* c) {
+    const char* e = std::getenv("SLM_GENERIC_ENGINE");
+    if (e && (!std::strcmp(e, "mr") || !std::strcmp(e, "gemm") || !std::strcmp(e, "bluestein"))) return false;
+    const long long elems = (long long)B * H * W;
+    c->rkey = rz_key(W, elems);
+    c->ckey = rz_key(H, elems);
+    if (c->rkey < 0 || c->ckey < 0) return false;
+    c->cw = rz_cw_of(c->ckey, W);
+    const int rpw = rz::rz_row_rpw(c->rkey);
+    return c->cw > 0 && rpw > 0 && H % rpw == 0;
+}
+
+// Stockham twiddle table of a plan key (the float32 engine's layout,
+// slm_capi.hip get_twiddles: every pass after the first holds (R - 1) Ns
+// entries exp(-2 pi i j r / (Ns R))) and the identity order (natural in and out)
+int rz_plan_line(GenericEngine* g, int key, mr::LinePlan* pl, hipStream_t st) {
+    const RadixPlan& rp = kPlans[key];
+    std::vector<double> tw;
+    int ns = 1;
+    for (int k = 0; k < rp.npass; ++k) {
+        const int r_ = rp.r[k];
+        if (ns > 1) {
+            const long long L = (long long)ns * r_;
+            for (int r = 1; r < r_; ++r)
+                for (int j = 0; j < ns; ++j) {
+                    const long long q = ((long long)j * r) % L;
+                    const double ang = -2.0 * M_PI * (double)q / (double)L;
+                    tw.push_back(std::cos(ang));
+                    tw.push_back(std::sin(ang));
+                }
+        }
+        ns *= r_;
+    }
+    if (tw.empty()) {
+        tw.push_back(1.0);
+        tw.push_back(0.0);
+    }
+    std::vector<int> rev(rp.n);
+    for (int e = 0; e < rp.n; ++e) rev[e] = e;
+    void *dtw = nullptr, *drev = nullptr;
+    if (hipMalloc(&dtw, tw.size() * sizeof(double)) != hipSuccess) return slm_set_error(SLM_ERR_HIP, "radix c128: allocation");
+    g->tables.push_back(dtw);
+    if (hipMalloc(&drev, rev.size() * sizeof(int)) != hipSuccess) return slm_set_error(SLM_ERR_HIP, "radix c128: allocation");
+    g->tables.push_back(drev);
+    G_HIP(hipMemcpyAsync(dtw, tw.data(), tw.size() * sizeof(double), hipMemcpyHostToDevice, st));
+    G_HIP(hipMemcpyAsync(drev, rev.data(), rev.size() * sizeof(int), hipMemcpyHostToDevice, st));
+    G_HIP(hipStreamSynchronize(st));
+    pl->n = rp.n;
+    pl->np = 0;
+    pl->tw = static_cast<const double2*>(dtw);
+    pl->rev = static_cast<const int*>(drev);
     return 0;
 }
 
@@ -533,6 +731,11 @@ int mr_row(GenericEngine* g, const GenericView& v, int op, mr::RowArgs a, int cl
     const int grid = v.B * ((v.H + g->rpw - 1) / g->rpw);
     const size_t lds = (size_t)g->rpw * v.W * sizeof(double2);
     Mark mk(v, cls);
+    if (g->rz) {
+        if (rz::rz_row_launch(g->rkey, op, a, grid, v.stream))
+            return slm_set_error(SLM_ERR_HIP, "complex128 radix row launch failed");
+        return 0;
+    }
     if (mr::mr_row_launch(op, g->big, a, grid, lds, v.stream))
         return slm_set_error(SLM_ERR_HIP, "mixed-radix row launch failed");
     return 0;
@@ -557,6 +760,11 @@ int mr_col(GenericEngine* g, const GenericView& v, int op, mr::ColArgs a, int cl
     const int grid = v.B * g->nwg_col;
     const size_t lds = ((size_t)v.H << g->cw_log2) * sizeof(double2);
     Mark mk(v, cls);
+    if (g->rz) {
+        if (rz::rz_col_launch(g->ckey, g->rz_cw, op, a, grid, v.stream))
+            return slm_set_error(SLM_ERR_HIP, "complex128 radix column launch failed");
+        return 0;
+    }
     if (mr::mr_col_launch(op, g->big, a, grid, lds, v.stream))
         return slm_set_error(SLM_ERR_HIP, "mixed-radix column launch failed");
     return 0;
@@ -655,6 +863,8 @@ int mr_enqueue(GenericEngine* g, const GenericView& v, int loops, double tol, in
 }  // namespace
 
 int generic_nwg(int B, int H, int W, long long holo) {
+    RzChoice rc;
+    if (rz_shape(B, H, W, &rc)) return W / rc.cw;
     if (mr_shape_ok(H, W)) {
         const MrTiling t = mr_tiling(B, H, W);
         return (W + (1 << t.cw_log2) - 1) >> t.cw_log2;
@@ -662,17 +872,20 @@ int generic_nwg(int B, int H, int W, long long holo) {
     return (int)std::max<long long>(1, std::min<long long>(1024, holo / (kGT * 8)));
 }
 
-bool generic_uses_blas(const GenericEngine* g) { return g && !g->mr; }
+bool generic_uses_blas(const GenericEngine* g) {
+    (void)g;  // no vendor library calls on any back end since r06: every run is graph-captured
+    return false;
+}
+
+int generic_kind(const GenericEngine* g) { return !g ? -1 : g->rz ? 4 : g->mr ? 3 : 2; }  // 2: line transforms
 
 void generic_destroy(GenericEngine* g) {
     if (!g) return;
-    for (void* p : {(void*)g->a, (void*)g->b, (void*)g->d, (void*)g->x, (void*)g->tmp, (void*)g->fw})
+    for (void* p : {(void*)g->a, (void*)g->b, (void*)g->d, (void*)g->x, (void*)g->tmp, (void*)g->tmp2})
         if (p) (void)hipFree(p);
     for (void* p : g->tables)
         if (p) (void)hipFree(p);
     if (g->ain_rev) (void)hipFree(g->ain_rev);
-    if (g->fh && g->fh != g->fw) (void)hipFree(g->fh);
-    if (g->blas) (void)rocblas_destroy_handle(g->blas);
     delete g;
 }
 
@@ -687,6 +900,25 @@ int generic_create(const GenericView& v, GenericEngine** out) {
     auto alloc = [&](double2** p, size_t count) {
         return hipMalloc((void**)p, count * sizeof(double2)) == hipSuccess;
     };
+    RzChoice rc;
+    if (rz_shape(v.B, v.H, v.W, &rc)) {  // complex128 radix plans: the mixed-radix buffers, Stockham tables
+        g->mr = g->rz = true;
+        g->rkey = rc.rkey;
+        g->ckey = rc.ckey;
+        g->rz_cw = rc.cw;
+        g->nwg_col = v.W / rc.cw;
+        g->rpw = rz::rz_row_rpw(rc.rkey);
+        if (g->nwg_col != v.nwg) return fail_free(slm_set_error(SLM_ERR_STATE, "radix c128: partial-slab mismatch"));
+        if (!alloc(&g->a, n) || !alloc(&g->b, n) || (v.algo == SLM_ALGO_GD && !alloc(&g->x, n)) ||
+            (v.has_ain && hipMalloc((void**)&g->ain_rev, (size_t)v.holo * sizeof(float)) != hipSuccess))
+            return fail_free(slm_set_error(SLM_ERR_HIP, "radix c128: device allocation failed"));
+        if (int e = rz_plan_line(g, rc.rkey, &g->pw, v.stream)) return fail_free(e);
+        if (int e = rz_plan_line(g, rc.ckey, &g->ph, v.stream)) return fail_free(e);
+        if (hipMemsetAsync(g->a, 0, n * sizeof(double2), v.stream) != hipSuccess)
+            return fail_free(slm_set_error(SLM_ERR_HIP, "radix c128: state initialisation failed"));
+        *out = g;
+        return 0;
+    }
     if (mr_shape_ok(v.H, v.W)) {  // mixed radix: two state buffers (+ the GD field), line plans
         g->mr = true;
         g->big = mr_big(v.H, v.W);
@@ -707,30 +939,13 @@ int generic_create(const GenericView& v, GenericEngine** out) {
         *out = g;
         return 0;
     }
-    if (!alloc(&g->a, n) || !alloc(&g->b, n) || !alloc(&g->d, n) || !alloc(&g->tmp, n) ||
-        (v.algo == SLM_ALGO_GD && !alloc(&g->x, n)) || !alloc(&g->fw, (size_t)v.W * v.W))
-        return fail_free(slm_set_error(SLM_ERR_HIP, "DFT engine: device allocation failed"));
-    {
-        const std::vector<double> m = dft_matrix(v.W);
-        if (hipMemcpyAsync(g->fw, m.data(), m.size() * sizeof(double), hipMemcpyHostToDevice, v.stream) !=
-                hipSuccess ||
-            hipStreamSynchronize(v.stream) != hipSuccess)
-            return fail_free(slm_set_error(SLM_ERR_HIP, "DFT engine: matrix upload failed"));
-    }
-    if (v.H == v.W) {
-        g->fh = g->fw;
-    } else {
-        if (!alloc(&g->fh, (size_t)v.H * v.H)) return fail_free(slm_set_error(SLM_ERR_HIP, "DFT engine: allocation"));
-        const std::vector<double> m = dft_matrix(v.H);
-        if (hipMemcpyAsync(g->fh, m.data(), m.size() * sizeof(double), hipMemcpyHostToDevice, v.stream) !=
-                hipSuccess ||
-            hipStreamSynchronize(v.stream) != hipSuccess)
-            return fail_free(slm_set_error(SLM_ERR_HIP, "DFT engine: matrix upload failed"));
-    }
-    if (rocblas_create_handle(&g->blas) != rocblas_status_success ||
-        rocblas_set_stream(g->blas, v.stream) != rocblas_status_success ||
-        rocblas_set_atomics_mode(g->blas, rocblas_atomics_not_allowed) != rocblas_status_success)
-        return fail_free(slm_set_error(SLM_ERR_HIP, "DFT engine: rocBLAS handle setup failed"));
+    if (!alloc(&g->a, n) || !alloc(&g->b, n) || !alloc(&g->d, n) || !alloc(&g->tmp, n) || !alloc(&g->tmp2, n) ||
+        (v.algo == SLM_ALGO_GD && !alloc(&g->x, n)))
+        return fail_free(slm_set_error(SLM_ERR_HIP, "line transforms: device allocation failed"));
+    const bool chirp_all = mr_forced_lines();
+    if (int rc = line_plan(g, v.W, chirp_all, &g->lw, &g->big_w, v.stream)) return fail_free(rc);
+    if (int rc = line_plan(g, v.H, chirp_all, &g->lh, &g->big_h, v.stream)) return fail_free(rc);
+    if (int rc = mr_roots(v.stream)) return fail_free(rc);
     *out = g;
     return 0;
 }

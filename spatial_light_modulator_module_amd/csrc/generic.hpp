@@ -1,11 +1,12 @@
 // Any-size engine of the GS / GD loops: image sides that no float32 radix plan
 // (plans.hpp) covers. The reference takes any (h, w) (src/algorithms.py:20-27;
 // scipy.fft handles every length), so such plans run in complex float64 with
-// row-major state: on hand-written mixed-radix transforms (mixed_radix.hpp)
-// where both sides factor into 2, 3, 5, 7, 11, 13, otherwise as products with
-// the dense DFT matrices (rocBLAS ZGEMM on the MI355X matrix cores) plus
-// element-wise kernels. slm_capi.hip owns the plan's buffers; this engine owns
-// its work buffers, line plans / DFT matrices and the rocBLAS handle.
+// row-major state: on the complex128 radix-plan kernels (radix_c128.hpp) where
+// both sides have a radix plan ($SLM_ENGINE=float64), on hand-written
+// mixed-radix transforms (mixed_radix.hpp) where both sides factor into 2, 3,
+// 5, 7, 11, 13, otherwise as 1-D line transforms (direct, or Bluestein's
+// chirp-z over a mixed-radix length) plus element-wise kernels. slm_capi.hip
+// owns the plan's buffers; this engine owns its work buffers and line plans.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -37,10 +38,13 @@ struct GenericView {
 };
 
 // statistics blocks per hologram (the partials' nwg): column tiles of the
-// mixed-radix back end, element chunks of the DFT-GEMM one
+// mixed-radix / radix-plan back ends, element chunks of the line-transform one
 int generic_nwg(int B, int H, int W, long long holo);
-// true for the DFT-GEMM back end (rocBLAS calls: runs are not graph-captured)
+// true for a back end whose runs cannot be graph-captured (none since r06,
+// when the rocBLAS DFT products gave way to the line transforms)
 bool generic_uses_blas(const GenericEngine* g);
+// back end: 2 line transforms (chirp-z), 3 mixed radix, 4 complex128 radix plans (slm_plan_engine codes)
+int generic_kind(const GenericEngine* g);
 int generic_create(const GenericView& v, GenericEngine** out);
 void generic_destroy(GenericEngine* g);
 // one full run (setup, loops iterations, phase and expected output, statistics),

@@ -278,6 +278,30 @@ __device__ __forceinline__ void fft_dit(double2* lds, const Lines& g, const Line
     }
 }
 
+// element-wise pieces shared by the mixed-radix kernels (mr_inst.hip) and the
+// complex128 radix-plan kernels (radix_c128.hpp): numpy's dtype rules of the
+// reference's loop
+__device__ __forceinline__ double amp_of(const void* tgt, int tt, long long i) {
+    if (tt == TGT_U8) return (double)TgtLoad<TGT_U8>::amp(TgtLoad<TGT_U8>::load(tgt, i));
+    return (double)(float)sqrt((double)static_cast<const float*>(tgt)[i]);  // numpy: sqrt(float32) is float32
+}
+__device__ __forceinline__ double t_of(const void* tgt, int tt, long long i) {
+    return tt == TGT_U8 ? (double)static_cast<const uint8_t*>(tgt)[i] : (double)static_cast<const float*>(tgt)[i];
+}
+// a exp(i angle(z)) == a z / |z|, angle(0) = 0 -> a (src/algorithms.py:30,33)
+__device__ __forceinline__ double2 unit_of(double2 z, double a) {
+    const double n2 = z.x * z.x + z.y * z.y;
+    if (n2 == 0.0) return make_double2(a, 0.0);
+    const double r = a / sqrt(n2);
+    return make_double2(z.x * r, z.y * r);
+}
+// x / |x| a (src/algorithms.py:84; |x| = 0 gives NaN as there)
+__device__ __forceinline__ double2 u_of(double2 x, double a) {
+    const double r = a / sqrt(x.x * x.x + x.y * x.y);
+    return make_double2(x.x * r, x.y * r);
+}
+__device__ __forceinline__ double2 round_c64(double2 z) { return make_double2((double)(float)z.x, (double)(float)z.y); }
+
 // ------------------------------------------------------------------------
 // kernels
 // ------------------------------------------------------------------------
@@ -340,6 +364,25 @@ struct ColArgs {
     long long holo = 0;
     LinePlan pl;                       // length H
 };
+
+// One 1-D transform per workgroup over rows of `n` complex128 (any n; the
+// any-size engine's transforms for sides with a prime factor above 13, and
+// their partner side): out[line] = DFT_n(in[line]), forward or the unscaled
+// inverse (computed as conj(DFT(conj x))). direct: n has a mixed-radix plan
+// `pl` -- DIF, then the digit reversal on the store. Otherwise Bluestein's
+// chirp-z: with w_j = exp(i pi j^2 / n), DFT_n(x)_k = conj(w_k) (a * b)_k for
+// a_j = x_j conj(w_j), b_j = w_j (j in (-n, n)), the circular convolution over
+// a mixed-radix length M = pl.n >= 2n - 1 as DIF -> times bhat (FFT_M(b) / M
+// in DIF output order) -> inverse DIT.
+struct LineArgs {
+    const double2* in = nullptr;
+    double2* out = nullptr;
+    int n = 0, direct = 1, inverse = 0;
+    LinePlan pl;                     // length n (direct) or M (Bluestein)
+    const double2* chirp = nullptr;  // w_j, j < n (Bluestein)
+    const double2* bhat = nullptr;   // FFT_M(b) / M, DIF order (Bluestein)
+};
+int mr_line_launch(bool big, const LineArgs& a, int lines, size_t lds, hipStream_t st);
 
 // host launchers (mr_inst.hip; big: a plan radix that is not small_radix; lds =
 // tile elements x 16 B; 0 or -1 on a launch error)

@@ -13,6 +13,10 @@
 // transforms gather their input in digit-reversed order and run a DIT.
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+#include <set>
+#include <utility>
+
 #include "mixed_radix.hpp"
 
 namespace slm {
@@ -24,27 +28,6 @@ namespace {
 // the odd radices 7, 11, 13
 template <bool BIG>
 constexpr int kWavesPerSimd = BIG ? 4 : 5;
-
-__device__ __forceinline__ double amp_of(const void* tgt, int tt, long long i) {
-    if (tt == TGT_U8) return (double)TgtLoad<TGT_U8>::amp(TgtLoad<TGT_U8>::load(tgt, i));
-    return (double)(float)sqrt((double)static_cast<const float*>(tgt)[i]);  // numpy: sqrt(float32) is float32
-}
-__device__ __forceinline__ double t_of(const void* tgt, int tt, long long i) {
-    return tt == TGT_U8 ? (double)static_cast<const uint8_t*>(tgt)[i] : (double)static_cast<const float*>(tgt)[i];
-}
-// a exp(i angle(z)) == a z / |z|, angle(0) = 0 -> a (src/algorithms.py:30,33)
-__device__ __forceinline__ double2 unit_of(double2 z, double a) {
-    const double n2 = z.x * z.x + z.y * z.y;
-    if (n2 == 0.0) return make_double2(a, 0.0);
-    const double r = a / sqrt(n2);
-    return make_double2(z.x * r, z.y * r);
-}
-// x / |x| a (src/algorithms.py:84; |x| = 0 gives NaN as there)
-__device__ __forceinline__ double2 u_of(double2 x, double a) {
-    const double r = a / sqrt(x.x * x.x + x.y * x.y);
-    return make_double2(x.x * r, x.y * r);
-}
-__device__ __forceinline__ double2 round_c64(double2 z) { return make_double2((double)(float)z.x, (double)(float)z.y); }
 
 template <int OP, bool BIG>
 __global__ void __launch_bounds__(kThreads, kWavesPerSimd<BIG>) mr_row_kernel(RowArgs a) {
@@ -230,24 +213,59 @@ __global__ void __launch_bounds__(kThreads, kWavesPerSimd<BIG>) mr_col_kernel(Co
     }
 }
 
-// dynamic LDS above 64 KiB must be allowed per kernel (once per process and kernel)
+// one line per workgroup (LineArgs, mixed_radix.hpp): a direct mixed-radix
+// transform, or Bluestein's chirp-z over a mixed-radix length M >= 2n - 1
+template <bool BIG>
+__global__ void __launch_bounds__(kThreads, kWavesPerSimd<BIG>) mr_line_kernel(LineArgs a) {
+    extern __shared__ double2 lds[];
+    const long long off = (long long)blockIdx.x * a.n;
+    const int M = a.pl.n;
+    const Lines g{1, M, 1};
+    auto cj = [&](double2 z) { return a.inverse ? make_double2(z.x, -z.y) : z; };  // inverse = conj DFT conj
+    if (a.direct) {
+        for (int e = threadIdx.x; e < a.n; e += kThreads) lds[e] = cj(a.in[off + e]);
+        __syncthreads();
+        fft_dif<false, false, BIG>(lds, g, a.pl);
+        for (int e = threadIdx.x; e < a.n; e += kThreads) a.out[off + a.pl.rev[e]] = cj(lds[e]);
+        return;
+    }
+    for (int e = threadIdx.x; e < M; e += kThreads)
+        lds[e] = e < a.n ? cmulc(cj(a.in[off + e]), a.chirp[e]) : make_double2(0.0, 0.0);  // x_j conj(w_j)
+    __syncthreads();
+    fft_dif<false, false, BIG>(lds, g, a.pl);
+    for (int e = threadIdx.x; e < M; e += kThreads) lds[e] = cmul(lds[e], a.bhat[e]);
+    __syncthreads();
+    fft_dit<true, false, BIG>(lds, g, a.pl);  // the circular convolution (1/M folded into bhat), natural order
+    for (int k = threadIdx.x; k < a.n; k += kThreads) a.out[off + k] = cj(cmulc(lds[k], a.chirp[k]));
+}
+
+// dynamic LDS above 64 KiB must be allowed per kernel and per device (the
+// attribute is a device's property: slm_gs_multi runs plans on several devices
+// from several host threads), once each
 template <class F>
 bool raise_lds(F fn) {
-    return hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLine * 16) ==
-           hipSuccess;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    static std::mutex mu;
+    static std::set<std::pair<const void*, int>> done;
+    std::lock_guard<std::mutex> lk(mu);
+    const auto key = std::make_pair((const void*)fn, dev);
+    if (done.count(key)) return true;
+    if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLine * 16) != hipSuccess)
+        return false;
+    done.insert(key);
+    return true;
 }
 
 template <int OP, bool BIG>
 int row_one(const RowArgs& a, int grid, size_t lds, hipStream_t st) {
-    static const bool ok = raise_lds(mr_row_kernel<OP, BIG>);
-    if (!ok) return -1;
+    if (!raise_lds(mr_row_kernel<OP, BIG>)) return -1;
     hipLaunchKernelGGL((mr_row_kernel<OP, BIG>), dim3(grid), dim3(kThreads), lds, st, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 template <int OP, bool BIG>
 int col_one(const ColArgs& a, int grid, size_t lds, hipStream_t st) {
-    static const bool ok = raise_lds(mr_col_kernel<OP, BIG>);
-    if (!ok) return -1;
+    if (!raise_lds(mr_col_kernel<OP, BIG>)) return -1;
     hipLaunchKernelGGL((mr_col_kernel<OP, BIG>), dim3(grid), dim3(kThreads), lds, st, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -302,6 +320,15 @@ int mr_col_occupancy(int op, bool big, size_t lds) {
     (void)op;
     return big ? occupancy_of(mr_col_kernel<CO_GS, true>, lds) : occupancy_of(mr_col_kernel<CO_GS, false>, lds);
 }
+int mr_line_launch(bool big, const LineArgs& a, int lines, size_t lds, hipStream_t st) {
+    auto go = [&](auto fn) {
+        if (!raise_lds(fn)) return -1;
+        hipLaunchKernelGGL(fn, dim3(lines), dim3(kThreads), lds, st, a);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    };
+    return big ? go(mr_line_kernel<true>) : go(mr_line_kernel<false>);
+}
+
 int mr_set_roots(const double2* roots, hipStream_t st) {
     if (hipMemcpyToSymbolAsync(HIP_SYMBOL(kRoots), roots, sizeof(kRoots), 0, hipMemcpyHostToDevice, st) != hipSuccess)
         return -1;

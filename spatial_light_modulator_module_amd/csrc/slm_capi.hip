@@ -381,8 +381,8 @@ struct slm_plan {
     // and relaunched as one graph -- 3 % per 1024^2 GS iteration, 6 % at 256^2
     // (gpurun_out/exp17: the inter-kernel gaps of 400 dependent launches)
     hipEvent_t marks[2] = {nullptr, nullptr};  // slm_plan_mark stopwatch
-    // sides without a radix plan: the DFT-GEMM engine (generic.hpp) runs the
-    // loop; state and arrays row-major, float64 arithmetic
+    // sides without a radix plan (or $SLM_ENGINE=float64): the any-size engine
+    // (generic.hpp) runs the loop; state and arrays row-major, float64 arithmetic
     GenericEngine* gen = nullptr;
     hipGraphExec_t gexec = nullptr;
     int g_loops = -1, g_checked = -1, g_state = -1;
@@ -810,7 +810,7 @@ int recover_grid_fault(slm_plan* p, bool* faulted) {
 }
 
 // GenericView::mark of timed runs: each marked launch between an event pair on
-// the plan stream (the DFT-GEMM / mixed-radix engine launches directly)
+// the plan stream (the any-size engine launches directly)
 int generic_mark(void* ctx, int cls, int begin) {
     slm_plan* p = static_cast<slm_plan*>(ctx);
     if (begin) {
@@ -1016,7 +1016,8 @@ int plan_create_on(int device, int algo, int batch, int height, int width, int t
     if (tgt_type != SLM_TGT_U8 && tgt_type != SLM_TGT_F32) return fail(SLM_ERR_ARG, "unknown target type");
     if (height < 1 || width < 1) return fail(SLM_ERR_ARG, "image shape %dx%d", height, width);
     // sides without a radix plan (plans.hpp) run the any-size engine (generic.hpp:
-    // mixed-radix kernels, DFT-GEMM for large prime factors). $SLM_ENGINE=float64
+    // mixed-radix kernels, chirp-z line transforms for large prime factors).
+    // $SLM_ENGINE=float64
     // sends every shape there: complex128 state and float64 arithmetic
     // throughout, the reference's own dtypes -- the radix plans keep complex64
     // between their passes, which sets GD's float64-butterfly floor at ~3e-5
@@ -1208,7 +1209,7 @@ int slm_plan_set_precision(slm_plan* p, int precision) {
     if (!p) return fail(SLM_ERR_ARG, "null plan");
     if (precision != SLM_PRECISION_F32 && precision != SLM_PRECISION_F64)
         return fail(SLM_ERR_ARG, "unknown precision %d", precision);
-    if (p->gen) return 0;  // the DFT-GEMM engine computes in float64 only
+    if (p->gen) return 0;  // the any-size engine computes in float64 only
     HIP_TRY(hipSetDevice(p->device));
     RC(configure(p, precision));
     return 0;
@@ -1445,7 +1446,7 @@ long long slm_plan_kernel_bytes(slm_plan* p, int cls) {
     const long long tb = p->tt == SLM_TGT_U8 ? 1 : 4;
     const long long ab = p->has_ain ? 4 : 0;
     if (p->gen) {
-        if (generic_uses_blas(p->gen)) return 0;  // DFT-GEMM: no column / row kernel classes
+        if (generic_kind(p->gen) == 2) return 0;  // line transforms: no column / row kernel classes
         // mixed radix, complex128 state: column pass in 16 + T + out 16 (GD statistics: in + T);
         // row pass in 16 + out 16 (+ a_in) (+ GD field read and write 32)
         switch (cls) {
@@ -1482,7 +1483,7 @@ int slm_plan_engine(slm_plan* p, int* col_engine, int* row_engine) {
     if (!p || !col_engine || !row_engine) return fail(SLM_ERR_ARG, "null argument");
     // mirrors kernels.hpp: kShuffle<K, P> && (CW == 2 | RPW == 2) && one line per thread
     if (p->gen) {
-        *col_engine = *row_engine = generic_uses_blas(p->gen) ? 2 : 3;  // DFT-GEMM / mixed radix (generic.hpp)
+        *col_engine = *row_engine = generic_kind(p->gen);  // line transforms / mixed radix / radix c128 (generic.hpp)
         return 0;
     }
     auto shuf = [&](int key, int prec) {
@@ -1627,7 +1628,7 @@ int slm_fft2(const float* in, float* out, int batch, int height, int width, int 
     const long long n = (long long)batch * p->holo;
     const size_t bytes = (size_t)n * sizeof(float2);
     int rc = 0;
-    if (p->gen) {  // DFT-GEMM engine: row-major in place through the staging buffer
+    if (p->gen) {  // any-size engine: row-major in place through the staging buffer
         hipError_t e = hipMemcpyAsync(p->xa, in, bytes, hipMemcpyHostToDevice, p->stream);
         if (e != hipSuccess) rc = fail(SLM_ERR_HIP, "upload failed: %s", hipGetErrorString(e));
         if (!rc) rc = generic_fft2(p->gen, gview(p), p->xa, p->xa, inverse);
@@ -1666,8 +1667,9 @@ int slm_fft2_c128(const double* in, double* out, int batch, int height, int widt
     if (batch < 1 || height < 1 || width < 1) return fail(SLM_ERR_ARG, "shape %d x %d x %d", batch, height, width);
     RC(ensure_device());
     HIP_TRY(hipSetDevice(g_device));
-    // the float64 engine of the any-size plans (mixed radix where the sides
-    // factor, else DFT-GEMM), whatever the shape: a scratch GS view of its own
+    // the float64 engine of the any-size plans (radix-plan kernels on 2^k / 768
+    // sides under $SLM_ENGINE=float64, mixed radix where the sides factor, else
+    // chirp-z line transforms), whatever the shape: a scratch GS view of its own
     slm_plan q;
     q.algo = SLM_ALGO_GS;
     q.B = batch;

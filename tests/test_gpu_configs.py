@@ -133,10 +133,11 @@ def test_gd_1024_configs2(gpu):
 @pytest.mark.gpu
 def test_gd_1024_configs2_at_500_float64_engine(gpu, monkeypatch):
     """configs[2] at its own 500 iterations within the north-star 1e-5 rms:
-    $SLM_ENGINE=float64 runs the any-size engine (complex128 state, float64
-    arithmetic, numpy's dtype rules) on the radix-plan shape. The float32
-    plan's floor there is ~7e-5 (test_gd_1024_configs2) and float64
-    butterflies over the radix plans' complex64 passes ~3e-5."""
+    $SLM_ENGINE=float64 runs the complex128 radix-plan kernels (radix_c128.hpp:
+    complex128 state, float64 arithmetic, numpy's dtype rules) on this
+    radix-plan shape. The float32 plan's floor there is ~7e-5
+    (test_gd_1024_configs2) and float64 butterflies over the radix plans'
+    complex64 passes ~3e-5."""
     from spatial_light_modulator_module_amd import algorithms as alg
 
     lib = gpu
@@ -145,7 +146,7 @@ def test_gd_1024_configs2_at_500_float64_engine(gpu, monkeypatch):
     x0 = alg.make_initial_guess("random", None, t, 42)
     monkeypatch.setenv("SLM_ENGINE", "float64")
     with lib.Plan(lib.ALGO_GD, 1, n, n, lib.TGT_F32, False, loops) as p:
-        assert p.engine()[0] in ("mixed-radix", "dft-gemm"), p.engine()
+        assert p.engine() == ("radix-c128", "radix-c128"), p.engine()
         p.set_target(t[None])
         p.set_field(x0[None])
         p.set_lr(np.full(loops, 0.005, np.float32))
@@ -162,31 +163,41 @@ def test_gd_1024_configs2_at_500_float64_engine(gpu, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.timeout(900)
-def test_gs_4096_at_200_float64_engine(gpu, monkeypatch):
+@pytest.mark.parametrize("k", [0, 1, 2])
+def test_gs_4096_at_200_float64_engine(gpu, monkeypatch, k):
     """configs[4]'s per-hologram run length (200 iterations) at 4096^2 within
-    1e-5 rms: the SURVEY.md 8c warm start (float64 oracle state after 30
-    cold iterations, then 200 more) on the float64 any-size engine
-    ($SLM_ENGINE=float64: complex128 throughout). The float32 plans are gated
-    at +100 (test_gs_4096_warm_start_gate): chaotic growth of their rounding
-    takes them past the bar by +200."""
+    1e-5 rms on bench targets 0-2: the SURVEY.md 8c warm start (float64 oracle
+    state after 30 cold iterations, then 200 more) on $SLM_ENGINE=float64 --
+    the complex128 radix-plan kernels (radix_c128.hpp: complex128 state,
+    float64 butterflies, complex128 exchanges, as the reference's loop). The
+    float32 plans are gated at +100 (test_gs_4096_warm_start_gate): chaotic
+    growth of their rounding takes them past the bar by +200."""
     lib = gpu
-    t = bench_targets(0, 1, 4096)[0]
+    t = bench_targets(k, 1, 4096)[0]
     phi30, _, _ = fast_f64.gerchberg_saxton_f64(t, 30)
     phi30 = phi30.astype(np.float32)
     ref, _, err = fast_f64.gerchberg_saxton_f64(t, 200, initial_phase=phi30)
+    err = np.asarray(err)
     monkeypatch.setenv("SLM_ENGINE", "float64")
     with lib.Plan(lib.ALGO_GS, 1, 4096, 4096, lib.TGT_F32, False, 200) as p:
-        assert p.engine()[0] == "mixed-radix", p.engine()
+        assert p.engine() == ("radix-c128", "radix-c128"), p.engine()
         p.set_target(t[None])
         p.set_phase(phi30[None])
         p.run(200)
         ph, _, st, _ = p.read(expected=False)
     rms = orc.phase_rms(ph[0], ref)
-    print(f"[parity] GS 4096^2 warm 30+200, float64 engine: phase rms {rms:.3e}")
+    rel = np.abs(st[0, :200, 3] / err - 1)
+    print(f"[parity] GS 4096^2 target {k} warm 30+200, complex128 engine: phase rms {rms:.3e}; error curve "
+          f"max rel {rel[:100].max():.1e} (first 100), {rel.max():.1e} (200)")
     assert rms < PHASE_RMS_TOL
-    # (numpy's float32 dtype rules for a float32 target's amplitude and expected
-    # output, where the oracle keeps float64: the curves agree to ~1.4e-6)
-    np.testing.assert_allclose(st[0, :200, 3], err, rtol=1e-5)
+    # Both sides are float64 loops whose transforms round differently (Stockham
+    # kernels vs pocketfft, ~1e-16 per step); the warm-started iteration amplifies
+    # that difference about x1.045 per iteration (DESIGN.md section 5) to ~1e-7 rms
+    # of phase after 200, which moves the late error values by up to ~1e-6
+    # relative. So the curves are gated at 1e-6 over the first 100 iterations,
+    # where that drift is still below it, and at 1e-5 over all 200.
+    assert rel[:100].max() < 1e-6
+    assert rel.max() < 1e-5
 
 
 _ORACLE_4096 = {}

@@ -1,13 +1,16 @@
 """Image shapes without a float32 radix plan: the any-size engine
-(csrc/generic.hip) on both of its transform back ends.
+(csrc/generic.hip) on both of its transform back ends for such sides.
 
 The reference takes any (h, w) (src/algorithms.py:20-27; scipy.fft handles
 every length). Sides outside SUPPORTED_LENGTHS run in complex128 state with
 float64 arithmetic: on the hand-written mixed-radix kernels
 (csrc/mixed_radix.hpp, mr_inst.hip) where both sides factor into 2..13, else
-as products with the DFT matrices on rocBLAS ZGEMM. Every test here runs on
-each back end (`engine` fixture; $SLM_GENERIC_ENGINE=gemm forces the
-products), and both are held to the faithful float64 oracle
+as 1-D line transforms along rows and transposed columns -- direct for a
+mixed-radix side, Bluestein's chirp-z over a mixed-radix length for a side
+with a larger prime factor (mr_line_kernel). Every test here runs on each
+back end (`engine` fixture; $SLM_GENERIC_ENGINE=bluestein forces the line
+transforms with chirp-z on every side), and both are held to the faithful
+float64 oracle
 (oracle/gs_gd_oracle.py, pinned to the reference goldens in
 test_oracle_golden.py) far inside the north-star bar: warm-start GS and GD
 phases at the float32 output's rounding (<= 1e-6 rms gated; the float32 FFT
@@ -34,14 +37,14 @@ def _smooth(n):
 def _expected_engine(shape, engine):
     if engine == "mixed-radix" and all(_smooth(n) and n <= 8192 for n in shape):
         return "mixed-radix"
-    return "dft-gemm"
+    return "bluestein"
 
 
-@pytest.fixture(params=["mixed-radix", "dft-gemm"])
+@pytest.fixture(params=["mixed-radix", "bluestein"])
 def engine(request, monkeypatch):
     """The back end the plans of one test are created on (read at plan creation)."""
-    if request.param == "dft-gemm":
-        monkeypatch.setenv("SLM_GENERIC_ENGINE", "gemm")
+    if request.param == "bluestein":
+        monkeypatch.setenv("SLM_GENERIC_ENGINE", "bluestein")
     else:
         monkeypatch.delenv("SLM_GENERIC_ENGINE", raising=False)
     yield request.param
@@ -69,7 +72,7 @@ def _gs(lib, t, loops, phase=None, tol=0.0, checked=False, engine="mixed-radix")
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shape", [(7, 33), (100, 60), (768, 1000), (1000, 1024), (97, 101)])
+@pytest.mark.parametrize("shape", [(7, 33), (100, 60), (768, 1000), (1000, 1024), (97, 101), (1, 13), (2053, 2)])
 def test_generic_fft2_vs_numpy(gpu, engine, shape):
     rng = np.random.default_rng(1)
     x = (rng.standard_normal((2,) + shape) + 1j * rng.standard_normal((2,) + shape)).astype(np.complex64)
@@ -78,7 +81,7 @@ def test_generic_fft2_vs_numpy(gpu, engine, shape):
         want = np.fft.ifft2(x.astype(np.complex128)) * (shape[0] * shape[1]) if inverse else np.fft.fft2(
             x.astype(np.complex128))
         err = np.max(np.abs(got - want)) / np.max(np.abs(want))
-        assert err < 1e-6, err  # complex64 output rounding; the products are float64
+        assert err < 1e-6, err  # complex64 output rounding; the transforms are float64
 
 
 @pytest.mark.gpu
@@ -272,13 +275,45 @@ def test_mixed_radix_gs_1080x1920_warm_start(gpu):
 
 
 @pytest.mark.gpu
-def test_prime_side_falls_back_to_dft_gemm(gpu, monkeypatch):
-    """A side with a prime factor above 13 keeps the DFT-GEMM back end."""
+def test_prime_side_runs_the_chirp_z_line_transforms(gpu, monkeypatch):
+    """A side with a prime factor above 13 runs the line transforms (its own
+    side by chirp-z, the other directly); 13-smooth shapes the mixed radix."""
     monkeypatch.delenv("SLM_GENERIC_ENGINE", raising=False)
     with gpu.Plan(gpu.ALGO_GS, 1, 97, 120, gpu.TGT_F32, False, 2) as p:
-        assert p.engine() == ("dft-gemm", "dft-gemm")
+        assert p.engine() == ("bluestein", "bluestein")
     with gpu.Plan(gpu.ALGO_GS, 1, 99, 120, gpu.TGT_F32, False, 2) as p:
         assert p.engine() == ("mixed-radix", "mixed-radix")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(97, 101), (1272, 96), (53, 1272)])
+def test_prime_sides_gs_gd_vs_oracle(gpu, monkeypatch, shape):
+    """Sides with a prime factor above 13 (97, 101; 1272 = 2^3 3 53) on the
+    default engine: the chirp-z line transforms (Bluestein over a 5-smooth
+    length >= 2n - 1, mr_line_kernel), O(N log N) like the reference's
+    pocketfft (src/algorithms.py:27,31,34), against the faithful float64
+    oracle -- GS by the SURVEY.md 8c warm start (30 + 30), GD from the random
+    guess (30 iterations)."""
+    from spatial_light_modulator_module_amd import algorithms as alg
+
+    monkeypatch.delenv("SLM_GENERIC_ENGINE", raising=False)
+    t = _target(shape, True, seed=31)
+    phi30, _, _ = orc.gerchberg_saxton_faithful(t, 30)
+    phi30 = phi30.astype(np.float32)
+    ref, _, ref_err = orc.gerchberg_saxton_faithful(t, 30, initial_phase=phi30)
+    ph, _, stats, _ = _gs(gpu, t[None], 30, phi30[None], engine="bluestein")
+    rms = orc.phase_rms(ph[0], ref)
+    tf = _target(shape, False, seed=32)
+    x0 = alg.make_initial_guess("random", None, tf, 42)
+    ref_gd, _, ref_gd_err, _ = orc.gradient_descent_faithful(tf, 30, 0.005, 1.0, 0, initial_field=x0)
+    ph_gd, _, errs, _, _ = alg.run_gd(tf[None], 30, np.full(30, 0.005), 1.0, initial_field=x0[None])
+    rms_gd = orc.phase_rms(ph_gd[0], ref_gd)
+    print(f"[parity] bluestein {shape}: GS u8 warm 30+30 phase rms {rms:.3e}; GD 30 iterations {rms_gd:.3e}")
+    assert rms < 1e-6
+    np.testing.assert_allclose(stats[0, :30, 3], ref_err, rtol=1e-6)
+    assert rms_gd < 1e-5  # the field crosses the C-ABI as complex64 (test_generic_gd_vs_oracle)
+    np.testing.assert_allclose(errs[0], ref_gd_err, rtol=1e-5)
+    alg.clear_plans()
 
 
 @pytest.mark.gpu

@@ -87,7 +87,8 @@ def test_warm_start_parity_large(gpu, n, span, u8, seed):
 def test_headline_on_the_float64_engine(gpu, monkeypatch, seed):
     """The headline configuration (GS 1024^2, +200 from the oracle's 30-iteration
     state, the bench's own targets) on $SLM_ENGINE=float64 -- complex128 state
-    and float64 arithmetic, as the reference -- lands ~30x inside the 1e-5
+    and float64 arithmetic, as the reference (the complex128 radix-plan kernels,
+    radix_c128.hpp) -- lands ~30x inside the 1e-5
     bar that the float32 plans meet with ~2x margin (measured 3.9e-7 /
     3.1e-7: the iteration is chaotic, so even float64 rounding differences
     from pocketfft grow over 200 iterations)."""
@@ -97,7 +98,7 @@ def test_headline_on_the_float64_engine(gpu, monkeypatch, seed):
         ref, _, ref_err = orc.gerchberg_saxton_faithful(t, 200, initial_phase=phi_w)
     monkeypatch.setenv("SLM_ENGINE", "float64")
     with gpu.Plan(gpu.ALGO_GS, 1, 1024, 1024, gpu.TGT_F32, False, 200) as p:
-        assert p.engine()[0] == "mixed-radix", p.engine()
+        assert p.engine() == ("radix-c128", "radix-c128"), p.engine()
     ph, err = _gpu_warm_run(gpu, t, phi_w, 200, gpu.PRECISION_F64)
     rms = orc.phase_rms(ph, ref)
     print(f"[parity] 1024^2 f32 target (seed {seed}), float64 engine: warm-start 30+200: phase rms {rms:.3e}")

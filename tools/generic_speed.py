@@ -1,10 +1,15 @@
 #!/usr/bin/env python3
-"""Per-iteration time of the any-size engine's two back ends (mixed radix and
-DFT-GEMM, image sides without a float32 radix plan) next to a radix-plan
-shape, GS (and GD), float32 targets, one hologram; per-kernel HIP-event times
-and the physical bytes of the mixed-radix launches.
+"""Per-iteration time of the any-size engine's back ends next to the default
+engine, GS (and GD), float32 targets, `--batch` holograms; per-kernel
+HIP-event times and the physical bytes of the complex128 launches.
 
-    python tools/generic_speed.py [--iters 50] [--shapes 1080x1920,...] [--engines mixed,gemm] [--gd]
+Engines: default (no override: float32 radix plans where the sides have one,
+else the any-size engine), rz ($SLM_ENGINE=float64: the complex128 radix-plan
+kernels on 2^k / 768 sides, mixed radix elsewhere), mr (the same with
+$SLM_GENERIC_ENGINE=mr), bluestein ($SLM_GENERIC_ENGINE=bluestein: the
+chirp-z line transforms on every side).
+
+    python tools/generic_speed.py [--iters 50] [--shapes 1080x1920,...] [--engines default,bluestein] [--gd] [--batch 1]
 """
 import argparse
 import os
@@ -17,9 +22,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from spatial_light_modulator_module_amd import _lib  # noqa: E402
 
 
-def one(h, w, iters, algo):
-    t = np.random.default_rng(1).uniform(0, 255, (1, h, w)).astype(np.float32)
-    with _lib.Plan(algo, 1, h, w, _lib.TGT_F32, False, iters) as p:
+def one(h, w, iters, algo, batch=1):
+    t = np.random.default_rng(1).uniform(0, 255, (batch, h, w)).astype(np.float32)
+    with _lib.Plan(algo, batch, h, w, _lib.TGT_F32, False, iters) as p:
         p.set_target(t)
         wa = 0.0
         if algo == _lib.ALGO_GD:
@@ -48,28 +53,33 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--shapes", default="1080x1920,1920x1080,1280x1024,1200x1920,1000x1000,768x1000,1024x1024")
-    ap.add_argument("--engines", default="mixed,gemm")
+    ap.add_argument("--engines", default="default,bluestein")
     ap.add_argument("--gd", action="store_true")
+    ap.add_argument("--gs", type=int, default=1, help="0: GD only (with --gd)")
+    ap.add_argument("--batch", type=int, default=1)
     o = ap.parse_args()
     _lib.init(0)
-    algos = [("GS", _lib.ALGO_GS)] + ([("GD", _lib.ALGO_GD)] if o.gd else [])
+    algos = ([("GS", _lib.ALGO_GS)] if o.gs else []) + ([("GD", _lib.ALGO_GD)] if o.gd else [])
     for sh in o.shapes.split(","):
         h, w = (int(v) for v in sh.split("x"))
         for engine in o.engines.split(","):
-            if engine == "gemm":
-                os.environ["SLM_GENERIC_ENGINE"] = "gemm"
-            else:
-                os.environ.pop("SLM_GENERIC_ENGINE", None)
+            env = {"default": {}, "mixed": {}, "rz": {"SLM_ENGINE": "float64"},
+                   "mr": {"SLM_ENGINE": "float64", "SLM_GENERIC_ENGINE": "mr"},
+                   "bluestein": {"SLM_ENGINE": "float64", "SLM_GENERIC_ENGINE": "bluestein"}}[engine]
+            for k in ("SLM_ENGINE", "SLM_GENERIC_ENGINE"):
+                os.environ.pop(k, None)
+            os.environ.update(env)
             for name, algo in algos:
-                eng, dt, kern = one(h, w, o.iters, algo)
-                flops = 2 * (w * w * h + h * h * w) * 8.0 if eng == "dft-gemm" else 0.0
+                eng, dt, kern = one(h, w, o.iters, algo, o.batch)
+                flops = 0.0
                 ks = ", ".join(f"{k} {v[0]:.2f} us ({v[1]:.0f} GB/s)" for k, v in kern.items())
-                print(f"{name} {h}x{w} ({eng}): {dt * 1e3:.4f} ms per iteration"
+                print(f"{name} {o.batch}x{h}x{w} ({eng}): {dt * 1e3:.4f} ms per iteration"
                       + (f", {flops / dt / 1e12:.1f} TFLOP/s float64 in the DFT products" if flops else "")
                       + (f"; {ks}" if ks else ""), flush=True)
-            if engine == "gemm" and all(n in (768,) or n & (n - 1) == 0 for n in (h, w)):
+            if engine == "bluestein" and all(n in (768,) or n & (n - 1) == 0 for n in (h, w)):
                 break  # radix-plan shape: one line is enough
     os.environ.pop("SLM_GENERIC_ENGINE", None)
+    os.environ.pop("SLM_ENGINE", None)
 
 
 if __name__ == "__main__":

@@ -9,6 +9,11 @@ for several arithmetic configurations of the two iteration kernels:
 and their kernel times (HIP events).
 
     python tools/parity_1024.py [--seeds 1024,1234,1235] [--configs f32,f64,col64,row64]
+                                [--shape 768x1024] [--u8]
+
+--u8 draws uint8 targets (default_rng(seed).integers(0, 256)), the CLI's
+input dtype (src/generate_hologram.py:102-110); --shape runs another image
+shape (768x1024 is the CLI's own SLM shape).
 """
 import argparse
 import os
@@ -23,13 +28,15 @@ from spatial_light_modulator_module_amd import _lib  # noqa: E402
 
 
 def run(t, phi_w, span, cfg):
+    h, w = t.shape
+    tt = _lib.TGT_U8 if t.dtype == np.uint8 else _lib.TGT_F32
     env = {"f32": (None, _lib.PRECISION_F32), "f64": (None, _lib.PRECISION_F64),
            "col64": ("f32", _lib.PRECISION_F64), "row64": ("f64", _lib.PRECISION_F32)}[cfg]
     if env[0]:
         os.environ["SLM_ROW_PRECISION"] = env[0]
     else:
         os.environ.pop("SLM_ROW_PRECISION", None)
-    with _lib.Plan(_lib.ALGO_GS, 1, 1024, 1024, _lib.TGT_F32, False, span) as p:
+    with _lib.Plan(_lib.ALGO_GS, 1, h, w, tt, False, span) as p:
         p.set_precision(env[1])  # the column kernels' (and, without the override, the rows') precision
         p.set_target(t[None])
         p.set_phase(np.asarray(phi_w, np.float32)[None])
@@ -47,17 +54,21 @@ def main():
     ap.add_argument("--seeds", default="1024,1234,1235")
     ap.add_argument("--configs", default="f32,f64,col64,row64")
     ap.add_argument("--span", type=int, default=200)
+    ap.add_argument("--shape", default="1024x1024")
+    ap.add_argument("--u8", action="store_true")
     o = ap.parse_args()
     _lib.init(0)
     workers = min(16, os.cpu_count() or 1)
     for seed in (int(s) for s in o.seeds.split(",")):
-        t = np.random.default_rng(seed).uniform(0, 255, (1024, 1024)).astype(np.float32)
+        h, w = (int(x) for x in o.shape.split("x"))
+        rng = np.random.default_rng(seed)
+        t = rng.integers(0, 256, (h, w)).astype(np.uint8) if o.u8 else rng.uniform(0, 255, (h, w)).astype(np.float32)
         with sfft.set_workers(workers):
             phi_w, _, _ = orc.gerchberg_saxton_faithful(t, 30)
             ref, _, _ = orc.gerchberg_saxton_faithful(t, o.span, initial_phase=phi_w)
         for cfg in o.configs.split(","):
             ph, k, eng = run(t, phi_w, o.span, cfg)
-            print(f"seed {seed} {cfg:>6s} ({eng[0]}/{eng[1]}): phase rms {orc.phase_rms(ph, ref):.3e}; "
+            print(f"{o.shape} {'u8' if o.u8 else 'f32'} seed {seed} {cfg:>6s} ({eng[0]}/{eng[1]}): phase rms {orc.phase_rms(ph, ref):.3e}; "
                   + ", ".join(f"{n} {v:.2f} us" for n, v in k.items()), flush=True)
 
 
