@@ -34,7 +34,7 @@ NUM_KERNEL_CLASSES = 4
 KERNEL_CLASS_NAMES = ("col_main", "row_main", "gd_stats", "other")
 
 # sides with a radix plan (the fused FFT kernels); any other side runs the
-# DFT-GEMM engine (generic.hip)
+# float64 any-size engine (generic.hip: mixed radix, or chirp-z line transforms)
 SUPPORTED_LENGTHS = (64, 128, 256, 512, 768, 1024, 2048, 4096)
 
 

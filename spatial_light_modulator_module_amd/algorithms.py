@@ -9,15 +9,27 @@ error_evolution)`` triple (float64 arrays and a list of np.float64). All
 iteration arithmetic runs in libslm_hip.so; this module only prepares inputs
 (dtype rules, initial guesses) and formats results.
 
-Differences that remain: for image sides in SUPPORTED_LENGTHS
-(the fused FFT kernels) the loop state lives in complex64 in HBM with float32
-butterflies, twiddles and projections by default (float64 butterflies per plan
-with Plan.set_precision or $SLM_PRECISION=f64), so phases match the float64
-reference to <= 1e-5 rms under the warm-start protocol of SURVEY.md 8c (float32
-margins measured in DESIGN.md section 5: 4.0e-6..6.0e-6 at 256^2-1024^2), not
-bitwise; any other shape runs the float64 DFT-GEMM engine (complex128
-state). A float64 target is carried as float32 on the device, with its max
-and sum of squares (the error's constant terms) kept exact in float64.
+Engines and the cost model (see DESIGN.md sections 1, 3 and 5):
+
+* image sides both in SUPPORTED_LENGTHS (2^k from 64 to 4096, and 768): the
+  fused FFT kernels, two launches per iteration, loop state in complex64 in
+  HBM; float32 butterflies, twiddles and projections for float32 targets
+  (GS 1024^2: ~0.017 ms per iteration), float64 butterflies for uint8 GS
+  targets (the CLI's input; ~0.019 ms) -- Plan.set_precision or
+  $SLM_PRECISION=f32|f64 overrides. Phases match the float64 reference to
+  <= 1e-5 rms under the warm-start protocol of SURVEY.md 8c, not bitwise;
+* $SLM_ENGINE=float64 on such sides: the complex128 radix-plan kernels
+  (complex128 state, float64 arithmetic, the reference's own dtypes; GS
+  4096^2 ~0.5 ms, GD 1024^2 ~0.05 ms per iteration);
+* any other shape whose sides factor into 2, 3, 5, 7, 11, 13 (1080 x 1920,
+  1280 x 1024, ...): the float64 mixed-radix kernels, complex128 state, two
+  launches per iteration (GS 1080 x 1920: ~0.08 ms per iteration);
+* a side with a larger prime factor (97, 1272 = 8 * 3 * 53, ...): float64
+  1-D line transforms along rows and transposed columns, Bluestein's chirp-z
+  for that side -- O(N log N), several launches per transform.
+
+A float64 target is carried as float32 on the device, with its max and sum of
+squares (the error's constant terms) kept exact in float64.
 """
 from __future__ import annotations
 
@@ -39,7 +51,8 @@ from ._lib import ALGO_GD, ALGO_GS, TGT_F32, TGT_U8
 def _check_shape(t: np.ndarray):
     """Any (h, w), as the reference (src/algorithms.py:20-27): sides in
     SUPPORTED_LENGTHS run the fused FFT kernels, every other shape the
-    float64 DFT-GEMM engine (csrc/generic.hip)."""
+    float64 any-size engine (csrc/generic.hip: mixed-radix kernels for
+    13-smooth sides, chirp-z line transforms otherwise)."""
     if t.ndim != 2:
         # the reference unpacks `w, l = demanded_output.shape` (src/algorithms.py:20)
         raise ValueError(f"too many values to unpack (expected 2): target has shape {t.shape}")

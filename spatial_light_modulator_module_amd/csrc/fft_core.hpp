@@ -91,6 +91,35 @@ constexpr double cos48(int q) {
     return kCos48[48 - q];
 }
 constexpr double sin48(int q) { return cos48(q - 12); }
+// cos(2 pi q / 240) (correctly rounded doubles, 60-digit decimal evaluation):
+// the constant twiddles of radices with a factor 5 (5, 10, 15, 20, 30, 60) --
+// the mixed-radix plans of SLM panel lengths (1080, 1920, 1200, 1280, ...).
+// Radices dividing 48 keep the 48ths above (their arithmetic is unchanged).
+constexpr double kCos240[61] = {
+                                 1.0, 0.9996573249755573, 0.9986295347545738, 0.996917333733128,
+                                 0.9945218953682733, 0.9914448613738104, 0.9876883405951378, 0.9832549075639546,
+                                 0.9781476007338057, 0.9723699203976766, 0.9659258262890683, 0.958819734868193,
+                                 0.9510565162951535, 0.9426414910921784, 0.9335804264972017, 0.9238795325112867,
+                                 0.9135454576426009, 0.9025852843498606, 0.8910065241883679, 0.8788171126619654,
+                                 0.8660254037844386, 0.8526401643540922, 0.838670567945424, 0.8241261886220157,
+                                 0.8090169943749475, 0.7933533402912352, 0.7771459614569709, 0.7604059656000309,
+                                 0.7431448254773942, 0.7253743710122876, 0.7071067811865476, 0.688354575693754,
+                                 0.6691306063588582, 0.6494480483301837, 0.6293203910498375, 0.6087614290087207,
+                                 0.5877852522924731, 0.5664062369248328, 0.5446390350150271, 0.5224985647159489,
+                                 0.5, 0.4771587602596084, 0.4539904997395468, 0.43051109680829514,
+                                 0.4067366430758002, 0.3826834323650898, 0.35836794954530027, 0.3338068592337709,
+                                 0.30901699437494745, 0.2840153447039226, 0.25881904510252074, 0.23344536385590542,
+                                 0.20791169081775934, 0.18223552549214744, 0.15643446504023087, 0.1305261922200516,
+                                 0.10452846326765347, 0.07845909572784494, 0.052335956242943835, 0.026176948307873153,
+                                 0.0};
+constexpr double cos240(int q) {
+    q = ((q % 240) + 240) % 240;
+    if (q <= 60) return kCos240[q];
+    if (q <= 120) return -kCos240[120 - q];
+    if (q <= 180) return -kCos240[q - 120];
+    return kCos240[240 - q];
+}
+constexpr double sin240(int q) { return cos240(q - 60); }
 
 // ------------------------------------------------------------------------
 // complex helpers; C = float2 or double2
@@ -125,19 +154,37 @@ __device__ __forceinline__ float2 to_c64(C v) { return make_float2((float)v.x, (
 template <int K, int R, bool INV, class C>
 __device__ __forceinline__ C twc(C a) {
     using S = Scalar<C>;
-    constexpr int q = ((48 / R) * K) % 48;
-    if constexpr (q == 0) {
-        return a;
-    } else if constexpr (q == 24) {
-        return mk<C>(-a.x, -a.y);
-    } else if constexpr (q == 12) {  // forward: * (-i)
-        return INV ? mk<C>(-a.y, a.x) : mk<C>(a.y, -a.x);
-    } else if constexpr (q == 36) {  // forward: * (+i)
-        return INV ? mk<C>(a.y, -a.x) : mk<C>(-a.y, a.x);
+    if constexpr (48 % R == 0) {
+        constexpr int q = ((48 / R) * K) % 48;
+        if constexpr (q == 0) {
+            return a;
+        } else if constexpr (q == 24) {
+            return mk<C>(-a.x, -a.y);
+        } else if constexpr (q == 12) {  // forward: * (-i)
+            return INV ? mk<C>(-a.y, a.x) : mk<C>(a.y, -a.x);
+        } else if constexpr (q == 36) {  // forward: * (+i)
+            return INV ? mk<C>(a.y, -a.x) : mk<C>(-a.y, a.x);
+        } else {
+            constexpr S c = (S)cos48(q);
+            constexpr S s = (S)(INV ? sin48(q) : -sin48(q));
+            return mk<C>(a.x * c - a.y * s, a.x * s + a.y * c);
+        }
     } else {
-        constexpr S c = (S)cos48(q);
-        constexpr S s = (S)(INV ? sin48(q) : -sin48(q));
-        return mk<C>(a.x * c - a.y * s, a.x * s + a.y * c);
+        static_assert(240 % R == 0, "constant twiddles of radices dividing 48 or 240");
+        constexpr int q = ((240 / R) * K) % 240;
+        if constexpr (q == 0) {
+            return a;
+        } else if constexpr (q == 120) {
+            return mk<C>(-a.x, -a.y);
+        } else if constexpr (q == 60) {
+            return INV ? mk<C>(-a.y, a.x) : mk<C>(a.y, -a.x);
+        } else if constexpr (q == 180) {
+            return INV ? mk<C>(a.y, -a.x) : mk<C>(-a.y, a.x);
+        } else {
+            constexpr S c = (S)cos240(q);
+            constexpr S s = (S)(INV ? sin240(q) : -sin240(q));
+            return mk<C>(a.x * c - a.y * s, a.x * s + a.y * c);
+        }
     }
 }
 
@@ -227,6 +274,55 @@ __device__ __forceinline__ void dft_split(C* v) {
 template <bool INV, class C>
 struct Dft<8, INV, C> {
     __device__ __forceinline__ static void run(C* v) { dft_split<2, 4, INV, C>(v); }
+};
+// radix 5 (the mixed-radix plans): y_0 = v_0 + s_1 + s_2, s_q = v_q + v_(5-q),
+// d_q = v_q - v_(5-q); y_1,4 = a_1 -/+ i b_1, y_2,3 = a_2 -/+ i b_2 (forward) with
+// a_1 = v_0 + c_1 s_1 + c_2 s_2, a_2 = v_0 + c_2 s_1 + c_1 s_2,
+// b_1 = n_1 d_1 + n_2 d_2, b_2 = n_2 d_1 - n_1 d_2 (c_q = cos, n_q = sin of 2 pi q / 5)
+template <bool INV, class C>
+struct Dft<5, INV, C> {
+    __device__ __forceinline__ static void run(C* v) {
+        using S = Scalar<C>;
+        constexpr S c1 = (S)cos240(48), c2 = (S)cos240(96), n1 = (S)sin240(48), n2 = (S)sin240(96);
+        const C s1 = cadd(v[1], v[4]), d1 = csub(v[1], v[4]);
+        const C s2 = cadd(v[2], v[3]), d2 = csub(v[2], v[3]);
+        const C a1 = mk<C>(v[0].x + c1 * s1.x + c2 * s2.x, v[0].y + c1 * s1.y + c2 * s2.y);
+        const C a2 = mk<C>(v[0].x + c2 * s1.x + c1 * s2.x, v[0].y + c2 * s1.y + c1 * s2.y);
+        const C b1 = mk<C>(n1 * d1.x + n2 * d2.x, n1 * d1.y + n2 * d2.y);
+        const C b2 = mk<C>(n2 * d1.x - n1 * d2.x, n2 * d1.y - n1 * d2.y);
+        // forward: -i b = (b.y, -b.x); inverse: +i b = (-b.y, b.x)
+        const C j1 = INV ? mk<C>(-b1.y, b1.x) : mk<C>(b1.y, -b1.x);
+        const C j2 = INV ? mk<C>(-b2.y, b2.x) : mk<C>(b2.y, -b2.x);
+        v[0] = mk<C>(v[0].x + s1.x + s2.x, v[0].y + s1.y + s2.y);
+        v[1] = cadd(a1, j1);
+        v[4] = csub(a1, j1);
+        v[2] = cadd(a2, j2);
+        v[3] = csub(a2, j2);
+    }
+};
+template <bool INV, class C>
+struct Dft<6, INV, C> {
+    __device__ __forceinline__ static void run(C* v) { dft_split<2, 3, INV, C>(v); }
+};
+template <bool INV, class C>
+struct Dft<10, INV, C> {
+    __device__ __forceinline__ static void run(C* v) { dft_split<2, 5, INV, C>(v); }
+};
+template <bool INV, class C>
+struct Dft<15, INV, C> {
+    __device__ __forceinline__ static void run(C* v) { dft_split<3, 5, INV, C>(v); }
+};
+template <bool INV, class C>
+struct Dft<20, INV, C> {
+    __device__ __forceinline__ static void run(C* v) { dft_split<4, 5, INV, C>(v); }
+};
+template <bool INV, class C>
+struct Dft<24, INV, C> {
+    __device__ __forceinline__ static void run(C* v) { dft_split<8, 3, INV, C>(v); }
+};
+template <bool INV, class C>
+struct Dft<30, INV, C> {
+    __device__ __forceinline__ static void run(C* v) { dft_split<6, 5, INV, C>(v); }
 };
 template <bool INV, class C>
 struct Dft<12, INV, C> {

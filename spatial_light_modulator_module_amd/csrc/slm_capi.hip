@@ -1050,6 +1050,14 @@ int plan_create_on(int device, int algo, int batch, int height, int width, int t
     if (!p->gd_fuse && p->gd_mode != GD_LIN) p->gd_mode = GD_TWO;
     if (p->gd_mode == GD_TWO || p->gd_mode == GD_LIN) p->gd_fuse = 0;
     if (const char* e = std::getenv("SLM_GD_FAULT_TEST")) p->skip_wg_plus1 = std::atoi(e);
+    // GS on uint8 targets -- the CLI's input (src/generate_hologram.py:102-110) --
+    // takes float64 butterflies by default: float32 measured 7.7e-6 (1024^2) and
+    // 8.2e-6 (768 x 1024, the CLI's own shape) of the 1e-5 bar at the +200 warm
+    // start, float64 rows alone still 8.5e-6 at 768 x 1024, float64 butterflies
+    // <= 3.3e-6 on all six targets (profiles/r06/u8_margin.txt), for ~3 us per
+    // iteration. Float32 targets (the bench's) keep float32; $SLM_PRECISION
+    // (f32 / f64) overrides both.
+    if (algo == SLM_ALGO_GS && tgt_type == SLM_TGT_U8) p->prec = PREC_F64;
     if (const char* e = std::getenv("SLM_PRECISION")) p->prec = (std::strcmp(e, "f64") == 0) ? PREC_F64 : PREC_F32;
     if (const char* e = std::getenv("SLM_ROW_PRECISION"))
         p->prec_row_force = (std::strcmp(e, "f64") == 0) ? PREC_F64 : PREC_F32;

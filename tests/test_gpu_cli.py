@@ -49,6 +49,43 @@ def test_gs_768x1024_warm_start_parity(gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("seed", [21, 22, 23])
+def test_gs_768x1024_u8_warm_start_200(gpu, seed):
+    """The CLI's own problem -- a uint8 768 x 1024 target (src/generate_hologram.py:
+    102-110, src/constants.py:5-6) -- at 200 warm-start iterations (SURVEY.md
+    8c) through the drop-in path (alg.run_gs, the plan's default precision:
+    float64 butterflies for uint8 targets since r06) held to 8e-6, and the
+    float32 butterflies (8.2e-6 measured on seed 21, profiles/r06/u8_margin.txt)
+    printed beside it and held to the 1e-5 bar."""
+    import os
+
+    import scipy.fft as sfft
+
+    from spatial_light_modulator_module_amd import algorithms as alg
+
+    t = np.random.default_rng(seed).integers(0, 256, (768, 1024)).astype(np.uint8)
+    with sfft.set_workers(min(16, os.cpu_count() or 1)):
+        phi30, _, _ = orc.gerchberg_saxton_faithful(t, 30)
+        want, _, err = orc.gerchberg_saxton_faithful(t, 200, initial_phase=phi30)
+    phase, _, errs, _, _ = alg.run_gs(t[None], 200, initial_phase=phi30[None].astype(np.float32))
+    rms = orc.phase_rms(phase[0], want)
+    with gpu.Plan(gpu.ALGO_GS, 1, 768, 1024, gpu.TGT_U8, False, 200) as p:
+        assert p.info()["precision"] == "f64", p.info()
+        p.set_precision(gpu.PRECISION_F32)
+        p.set_target(t[None])
+        p.set_phase(phi30[None].astype(np.float32))
+        p.run(200)
+        ph32 = p.read(expected=False, stats=False, iters=False)[0][0]
+    rms32 = orc.phase_rms(ph32, want)
+    print(f"[parity] GS 768x1024 u8 (seed {seed}) warm start 30+200: default (f64 butterflies) phase rms {rms:.3e}, "
+          f"f32 butterflies {rms32:.3e}")
+    assert rms < 8e-6
+    assert rms32 < PHASE_RMS_TOL
+    np.testing.assert_allclose(errs[0], err, rtol=1e-4)
+
+
+@pytest.mark.gpu
 def test_generate_hologram_cli_gs_with_deflect(gpu, tmp_path, monkeypatch):
     from spatial_light_modulator_module_amd import generate_hologram as gh
     from spatial_light_modulator_module_amd.algorithms import gerchberg_saxton

@@ -27,9 +27,11 @@ WORKERS = min(16, os.cpu_count() or 1)  # the GPU box gives a process a 16-CPU s
 
 
 def _gpu_warm_run(lib, t, phi_w, span, precision):
+    """precision None: the plan's default (float32; float64 butterflies for uint8 targets)"""
     tt = lib.TGT_U8 if t.dtype == np.uint8 else lib.TGT_F32
     with lib.Plan(lib.ALGO_GS, 1, t.shape[0], t.shape[1], tt, False, span) as p:
-        p.set_precision(precision)
+        if precision is not None:
+            p.set_precision(precision)
         p.set_target(t[None])
         p.set_phase(np.asarray(phi_w, np.float32)[None])
         p.run(span)
@@ -51,9 +53,9 @@ def test_reference_goldens_both_precisions(gpu, golden_dir, name, prec):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,span,u8,seed", [(1024, 200, True, 1024), (1024, 200, False, 1024),
-                                            (1024, 200, False, 1234), (1024, 200, False, 1235),
-                                            (2048, 100, False, 2048)])
+@pytest.mark.parametrize("n,span,u8,seed", [(1024, 200, True, 1024), (1024, 200, True, 1025), (1024, 200, True, 1026),
+                                            (1024, 200, False, 1024), (1024, 200, False, 1234),
+                                            (1024, 200, False, 1235), (2048, 100, False, 2048)])
 def test_warm_start_parity_large(gpu, n, span, u8, seed):
     """(1024, 200, float32 target) is the bench headline itself (BASELINE.json
     configs[1]), gated on three targets: default_rng(1024) and the bench's own
@@ -62,7 +64,12 @@ def test_warm_start_parity_large(gpu, n, span, u8, seed):
     axes, 2-column tiles, the narrow layout pair (8-wide X, 2-wide Y panels),
     i.e. col_kernel<11, 2, GS_MAIN, f32 target, f32, narrow> -- on the
     wave-shuffle transform pair (fft_shuffle.hpp) in both kernels, so the gate
-    covers the exact instantiation the roofline is quoted on."""
+    covers the exact instantiation the roofline is quoted on.
+
+    uint8 targets (the CLI's input dtype, src/generate_hologram.py:102-110)
+    on three targets: the plan's default there -- float64 butterflies since
+    r06 -- is held to 8e-6 (float32 measured up to 7.7e-6 of the 1e-5 bar,
+    profiles/r06/u8_margin.txt), float32 and float64 each to the bar."""
     rng = np.random.default_rng(seed)
     t = rng.integers(0, 256, (n, n)).astype(np.uint8) if u8 else rng.uniform(0, 255, (n, n)).astype(np.float32)
     with sfft.set_workers(WORKERS):
@@ -73,12 +80,16 @@ def test_warm_start_parity_large(gpu, n, span, u8, seed):
             info = p.info()
         assert (info["row_plan"], info["col_plan"], info["col_cw"], info["layout"], info["precision"],
                 info["engine"]) == (11, 11, 2, (8, 2), "f32", ("shuffle", "shuffle")), info
-    for prec, precision in (("f64", gpu.PRECISION_F64), ("f32", gpu.PRECISION_F32)):
+    if u8:
+        with gpu.Plan(gpu.ALGO_GS, 1, n, n, gpu.TGT_U8, False, span) as p:
+            assert p.info()["precision"] == "f64", p.info()
+    runs = [("f64", gpu.PRECISION_F64), ("f32", gpu.PRECISION_F32)] + ([("default", None)] if u8 else [])
+    for prec, precision in runs:
         ph, err = _gpu_warm_run(gpu, t, phi_w, span, precision)
         rms = orc.phase_rms(ph, ref)
         print(f"[parity] {n}^2 {'u8' if u8 else 'f32'} target (seed {seed}), {prec}: warm-start 30+{span}: "
               f"phase rms {rms:.3e}")
-        assert rms < PHASE_RMS_TOL
+        assert rms < (8e-6 if prec == "default" else PHASE_RMS_TOL)
         np.testing.assert_allclose(err, ref_err, rtol=1e-4)
 
 
