@@ -132,6 +132,21 @@ def pmc_traffic(config_key: str):
         return None
 
 
+def traffic_for_plan(traffic, info):
+    """The committed PMC entry only if it was collected on the plan being timed:
+    entries stamped by tools/pmc_traffic.py with [row plan, col plan, col tile,
+    precision, engines] must match (else None); unstamped (pre-r06) entries are
+    used as they are, flagged plan_checked False."""
+    if not traffic:
+        return traffic
+    want = [info.get("row_plan"), info.get("col_plan"), info.get("col_cw"), info.get("precision"),
+            list(info.get("engine", ()))]
+    got = traffic.get("plan")
+    if got is None:
+        return dict(traffic, plan_checked=False)
+    return dict(traffic, plan_checked=True) if list(got) == want else None
+
+
 def rocprof_kernels(config_key: str):
     """The committed rocprofv3 kernel-trace summary of this configuration
     (profiles/rocprof_kernels.json, written by tools/frac_check.py from a
@@ -304,6 +319,7 @@ def secondary(n, batch, iters, algo=_lib.ALGO_GS, precision=None, reps=3, width=
     # rocprofv3 PMC, profiles/ (keyed by engine too: complex128 plans move other bytes)
     eng_tag = "" if plan_engine[0] in ("stockham", "shuffle") else "_" + plan_engine[0]
     traffic = pmc_traffic(f"{name}_{n}x{w}_b{batch}_it{iters}_{info['precision']}{eng_tag}")
+    traffic = traffic_for_plan(traffic, info)
     for k, row in rows.items():
         row["traffic_bytes_per_launch"] = None if traffic is None else traffic.get(k)
     per_px = 76 if algo == _lib.ALGO_GD else 68
@@ -312,7 +328,7 @@ def secondary(n, batch, iters, algo=_lib.ALGO_GS, precision=None, reps=3, width=
     # iteration's launches (GS: a column and a row launch; GD: the column
     # launches and the row launch) over the measured iteration time
     pmc_frac = None
-    if traffic and all(traffic.get(k) for k in rows):
+    if traffic and all(traffic.get(k) for k in rows):  # (plan-checked above)
         pmc_frac = round(sum(traffic[k] for k in rows) / iter_s / 1e9 / HBM_PEAK_GBS, 4)
     return {"algo": name, "shape": [batch, n, w], "iters": iters, "engine": list(plan_engine),
             "iter_frac_of_hbm_peak_pmc": pmc_frac,
@@ -489,7 +505,7 @@ def main():
 
     prec = info["precision"]  # butterflies / twiddles / exchanges; HBM state is complex64
     key = f"gs_{n}x{n}_b{bper}_it{iters}_{prec}"
-    traffic = pmc_traffic(key)
+    traffic = traffic_for_plan(pmc_traffic(key), info)
     dr = rows[dom]
     iter_s = ms_per_step / iters / 1e3
     roofline = {"bound": "hbm", "achieved": round(dr["achieved_gbs"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -190,6 +190,9 @@ int slm_fft2(const float* in_re_im, float* out_re_im, int batch, int height, int
  * chirp-z line transforms) -> the float64 scipy.fft.ifft2 of move_traps.update_hologram,
  * src/move_traps.py:66 (times h w) */
 int slm_fft2_c128(const double* in_re_im, double* out_re_im, int batch, int height, int width, int inverse);
+/* frees the float64 engines slm_fft2_c128 keeps per (device, batch, h, w)
+ * (a few shapes; the drop-in's clear_plans calls it) */
+int slm_release_caches(void);
 
 /* ---- multi-GPU (one process per GPU, RCCL over xGMI) ------------------- */
 int slm_comm_unique_id(unsigned char* id128);

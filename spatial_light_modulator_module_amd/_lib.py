@@ -102,6 +102,7 @@ _SIGNATURES = [
     ("slm_transform_hologram", _c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp]),
     ("slm_fft2_intensity", _c_int, [_vp, _c_int, _c_int, _c_int, _vp]),
     ("slm_fft2_c128", _c_int, [_vp, _vp, _c_int, _c_int, _c_int, _c_int]),
+    ("slm_release_caches", _c_int, []),
 ]
 
 TRANSFORM_DEFLECT = 1
@@ -416,6 +417,12 @@ def fft2_c128(x: np.ndarray, inverse: bool = False) -> np.ndarray:
     check(load().slm_fft2_c128(ptr(a.view(np.float64)), ptr(out.view(np.float64)), b, h, w, int(bool(inverse))),
           "slm_fft2_c128")
     return out
+
+
+def release_caches() -> None:
+    """Free the float64 engines slm_fft2_c128 keeps per shape (no-op without a library)."""
+    if _lib is not None:
+        check(_lib.slm_release_caches(), "slm_release_caches")
 
 
 def transform_hologram(hologram, height, width, deflect_params=None, lens_params=None):

@@ -164,6 +164,7 @@ def get_plan(algo, batch, h, w, tgt_type, has_ain, max_loops) -> _lib.Plan:
 def clear_plans():
     while _PLANS:
         _PLANS.popitem()[1].close()
+    _lib.release_caches()  # slm_fft2_c128's per-shape engines (move_traps.update_hologram)
 
 
 # ---------------------------------------------------------------------------

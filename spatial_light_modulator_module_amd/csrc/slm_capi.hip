@@ -1670,15 +1670,49 @@ int slm_fft2(const float* in, float* out, int batch, int height, int width, int 
     return rc;
 }
 
-int slm_fft2_c128(const double* in, double* out, int batch, int height, int width, int inverse) {
-    if (!in || !out) return fail(SLM_ERR_ARG, "null argument");
-    if (batch < 1 || height < 1 || width < 1) return fail(SLM_ERR_ARG, "shape %d x %d x %d", batch, height, width);
-    RC(ensure_device());
-    HIP_TRY(hipSetDevice(g_device));
-    // the float64 engine of the any-size plans (radix-plan kernels on 2^k / 768
-    // sides under $SLM_ENGINE=float64, mixed radix where the sides factor, else
-    // chirp-z line transforms), whatever the shape: a scratch GS view of its own
-    slm_plan q;
+}  // extern "C"
+
+namespace {
+// slm_fft2_c128's float64 engines, cached per (device, batch, h, w) like the
+// drop-in's plans: move_traps.update_hologram calls it for every non-blank
+// image of the interactive trap loop, which rebuilt stream, buffers, line
+// plans and tables each time before r06. A few shapes are kept (oldest out);
+// slm_release_caches frees them (algorithms.clear_plans).
+struct C128Entry {
+    int device = 0, batch = 0, h = 0, w = 0;
+    slm_plan* q = nullptr;  // scratch GS view: its stream and engine only
+    double2* buf = nullptr;
+};
+std::mutex g_c128_mu;
+std::vector<C128Entry> g_c128;
+constexpr size_t kC128CacheMax = 4;
+
+void c128_free(C128Entry& e) {
+    if (e.buf) (void)hipFree(e.buf);
+    e.buf = nullptr;
+    free_plan(e.q);  // waits for its stream, frees the engine
+    e.q = nullptr;
+}
+
+int c128_entry(int batch, int height, int width, C128Entry** out) {
+    for (auto& e : g_c128)
+        if (e.device == g_device && e.batch == batch && e.h == height && e.w == width) {
+            *out = &e;
+            return 0;
+        }
+    if (g_c128.size() >= kC128CacheMax) {
+        (void)hipSetDevice(g_c128.front().device);
+        c128_free(g_c128.front());
+        g_c128.erase(g_c128.begin());
+        HIP_TRY(hipSetDevice(g_device));
+    }
+    C128Entry e;
+    e.device = g_device;
+    e.batch = batch;
+    e.h = height;
+    e.w = width;
+    e.q = new slm_plan();
+    slm_plan& q = *e.q;
     q.algo = SLM_ALGO_GS;
     q.B = batch;
     q.H = height;
@@ -1687,23 +1721,54 @@ int slm_fft2_c128(const double* in, double* out, int batch, int height, int widt
     q.max_loops = 1;
     q.nwg = generic_nwg(batch, height, width, q.holo);
     q.device = g_device;
-    HIP_TRY(hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking));
-    const size_t bytes = (size_t)batch * q.holo * sizeof(double2);
-    double2* buf = nullptr;
-    GenericEngine* g = nullptr;
     int rc = 0;
-    if (hipMalloc(&buf, bytes) != hipSuccess) rc = fail(SLM_ERR_HIP, "fft2_c128: allocation of %zu bytes", bytes);
-    if (!rc) rc = generic_create(gview(&q), &g);
-    if (!rc && hipMemcpyAsync(buf, in, bytes, hipMemcpyHostToDevice, q.stream) != hipSuccess)
-        rc = fail(SLM_ERR_HIP, "fft2_c128: upload failed");
-    if (!rc) rc = generic_fft2_z(g, gview(&q), buf, buf, inverse);
-    if (!rc) rc = copy_sync(out, buf, bytes, hipMemcpyDeviceToHost, q.stream);
-    (void)hipStreamSynchronize(q.stream);
-    generic_destroy(g);
-    if (buf) (void)hipFree(buf);
-    (void)hipStreamDestroy(q.stream);
-    q.stream = nullptr;
-    return rc;
+    if (hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking) != hipSuccess)
+        rc = fail(SLM_ERR_HIP, "fft2_c128: stream creation failed");
+    const size_t bytes = (size_t)batch * q.holo * sizeof(double2);
+    if (!rc && hipMalloc(&e.buf, bytes) != hipSuccess) rc = fail(SLM_ERR_HIP, "fft2_c128: allocation of %zu bytes", bytes);
+    if (!rc) rc = generic_create(gview(&q), &q.gen);
+    if (rc) {
+        c128_free(e);
+        return rc;
+    }
+    g_c128.push_back(e);
+    *out = &g_c128.back();
+    return 0;
+}
+}  // namespace
+
+extern "C" {
+
+int slm_fft2_c128(const double* in, double* out, int batch, int height, int width, int inverse) {
+    if (!in || !out) return fail(SLM_ERR_ARG, "null argument");
+    if (batch < 1 || height < 1 || width < 1) return fail(SLM_ERR_ARG, "shape %d x %d x %d", batch, height, width);
+    RC(ensure_device());
+    HIP_TRY(hipSetDevice(g_device));
+    // the float64 engine of the any-size plans (radix-plan kernels on 2^k / 768
+    // sides, mixed radix where the sides factor, else chirp-z line
+    // transforms), whatever the shape, cached per shape
+    std::lock_guard<std::mutex> lk(g_c128_mu);
+    C128Entry* e = nullptr;
+    RC(c128_entry(batch, height, width, &e));
+    slm_plan& q = *e->q;
+    const size_t bytes = (size_t)batch * q.holo * sizeof(double2);
+    if (hipMemcpyAsync(e->buf, in, bytes, hipMemcpyHostToDevice, q.stream) != hipSuccess)
+        return fail(SLM_ERR_HIP, "fft2_c128: upload failed");
+    RC(generic_fft2_z(q.gen, gview(&q), e->buf, e->buf, inverse));
+    return copy_sync(out, e->buf, bytes, hipMemcpyDeviceToHost, q.stream);
+}
+
+int slm_release_caches(void) {
+    std::lock_guard<std::mutex> lk(g_c128_mu);
+    int dev = 0;
+    const bool have = hipGetDevice(&dev) == hipSuccess;
+    for (auto& e : g_c128) {
+        (void)hipSetDevice(e.device);
+        c128_free(e);
+    }
+    g_c128.clear();
+    if (have) (void)hipSetDevice(dev);
+    return 0;
 }
 
 int slm_fft2_intensity(const float* phase, int batch, int height, int width, float* intensity_out) {
