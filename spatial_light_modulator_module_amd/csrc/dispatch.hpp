@@ -34,7 +34,7 @@ SLM_DECLARE_LENGTH(12)
 SLM_DECLARE_LENGTH(13)
 
 // plan keys (indices into kPlans); the Makefile builds one object per key
-static_assert(kNumPlans == 14, "update SLM_DECLARE_LENGTH / SLM_FOR_EACH_LENGTH and the Makefile");
+static_assert(kNumF32Plans == 14, "update SLM_DECLARE_LENGTH / SLM_FOR_EACH_LENGTH and the Makefile");
 #define SLM_FOR_EACH_LENGTH(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13)
 
 inline RowFn row_fn(int n, int mode, int prec, int lid = 0) {

@@ -434,13 +434,14 @@ struct TwCountOf<N, IntList<Rs...>> {
 //  split radix-16 twiddles w^(4a) w^b were measured: faster variants moved
 //  the 4096^2 float32 warm-start parity past the bar, slower ones were slower;
 //  DESIGN.md sections 4-5.)
-enum TwMode : int { TW_CACHED = 0, TW_DIRECT = 1 };
+enum TwMode : int { TW_CACHED = 0, TW_DIRECT = 1, TW_DIRECT_LAUNDER = 2 };
 
 template <int N, class C, int MODE>
 struct Twiddles;
 
 template <int N, class C>
 struct Twiddles<N, C, TW_CACHED> {
+    static constexpr bool kAlwaysLaunder = false;
     static constexpr int COUNT = TwCountOf<N, RadicesOf<N>>::value > 0 ? TwCountOf<N, RadicesOf<N>>::value : 1;
     C w[COUNT];
     __device__ __forceinline__ void launder() {}
@@ -455,6 +456,7 @@ struct Twiddles<N, C, TW_CACHED> {
 };
 template <int N, class C>
 struct Twiddles<N, C, TW_DIRECT> {
+    static constexpr bool kAlwaysLaunder = false;
     struct alignas(2 * sizeof(Scalar<C>)) Pod {  // trivially copyable twin of C
         Scalar<C> x, y;
     };
@@ -478,6 +480,14 @@ struct Twiddles<N, C, TW_DIRECT> {
             u[r] = INV ? cmulc(u[r], t) : cmul(u[r], t);
         });
     }
+};
+// TW_DIRECT whose loads are laundered before every transform whatever E (the
+// complex128 radix-plan kernels: a fused pair's second transform would
+// otherwise keep the first one's float64 twiddle loads live across the
+// element-wise epilogue -- 162 against 128 VGPRs for 4096-point E = 8 rows)
+template <int N, class C>
+struct Twiddles<N, C, TW_DIRECT_LAUNDER> : Twiddles<N, C, TW_DIRECT> {
+    static constexpr bool kAlwaysLaunder = true;
 };
 template <int N, class C, int MODE, int E, int Ns, int TwOff, int RegOff, int PowOff, int R, int... Rest>
 __device__ __forceinline__ void load_twiddles_pass(Twiddles<N, C, MODE>& tw, int t, const C* __restrict__ table) {
@@ -506,9 +516,9 @@ __device__ __forceinline__ void load_twiddles_impl(Twiddles<N, C, MODE>& tw, int
 }
 template <int N, class C, int MODE>
 __device__ __forceinline__ void load_twiddles(Twiddles<N, C, MODE>& tw, int t, const void* table) {
-    if constexpr (MODE == TW_DIRECT)
+    if constexpr (MODE == TW_DIRECT || MODE == TW_DIRECT_LAUNDER)
         tw.table = (typename Twiddles<N, C, MODE>::GlobalPtr)table;
-    if constexpr (MODE != TW_DIRECT)
+    if constexpr (MODE == TW_CACHED)
         load_twiddles_impl<N, C, MODE>(tw, t, static_cast<const C*>(table), RadicesOf<N>{});
 }
 
@@ -651,7 +661,7 @@ template <int K, bool INV, class C, int L, class V, class Lds, class Tw, class S
 __device__ __forceinline__ void stockham_all(V (&v)[L][PlanOf<K>::E], int t, const Tw& tw0, const Lds& lds,
                                              Sink& sink, IntList<Rs...>) {
     Tw tw = tw0;
-    if constexpr (kLaunder<K>) tw.launder();
+    if constexpr (kLaunder<K> || Tw::kAlwaysLaunder) tw.launder();
     stockham_from<PlanOf<K>::N, PlanOf<K>::E, L, INV, 1, 0, 0, 0, C, V, Lds, Tw, Sink, Rs...>(v, t, tw, lds, sink);
 }
 // passes 1.. of a transform whose first pass already wrote the LDS line
@@ -661,7 +671,7 @@ __device__ __forceinline__ void stockham_after_first(V (&v)[L][PlanOf<K>::E], in
                                                      Sink& sink, IntList<R0, Rs...>) {
     static_assert(sizeof...(Rs) > 0, "fused transforms need at least two passes");
     Tw tw = tw0;
-    if constexpr (kLaunder<K>) tw.launder();
+    if constexpr (kLaunder<K> || Tw::kAlwaysLaunder) tw.launder();
     stockham_from<PlanOf<K>::N, PlanOf<K>::E, L, INV, R0, 0, 0, 0, C, V, Lds, Tw, Sink, Rs...>(v, t, tw, lds, sink);
 }
 

@@ -50,6 +50,8 @@ struct GenericEngine {
     bool rz = false;
     int rkey = -1, ckey = -1;  // plan keys (plans.hpp) of the row / column transforms
     int rz_cw = 0;             // columns per column tile
+    int rz_lay = 0;            // state layout between the passes (radix_c128.hpp LAY_RM / LAY_B2)
+    float* tgt_blk = nullptr;  // the target as float in the radix kernels' B2 layout (rebuilt per run)
     bool big = false;        // a radix outside mr::small_radix in either plan (7, 11, 13)
     mr::LinePlan pw, ph;     // row (length W) and column (length H) transforms
     int rpw = 1;             // rows per row tile
@@ -169,6 +171,18 @@ __global__ void __launch_bounds__(kGT) k_ain_rev(const float* ain, float* out, c
     for (long long i = blockIdx.x * (long long)kGT + threadIdx.x; i < n; i += (long long)gridDim.x * kGT) {
         const long long r = i / W;
         out[i] = ain[r * W + rev[(int)(i - r * W)]];
+    }
+}
+// the target (uint8 or float32, row-major) as float in the complex128 radix
+// kernels' B2 layout (radix_c128.hpp, b2_index): the column passes' reads of it
+// are then contiguous like their field reads
+__global__ void __launch_bounds__(kGT) k_tgt_b2(const void* tgt, int tt, float* out, int H, int W, long long n) {
+    const long long holo = (long long)H * W;
+    for (long long i = blockIdx.x * (long long)kGT + threadIdx.x; i < n; i += (long long)gridDim.x * kGT) {
+        const long long b = i / holo, r = i - b * holo;
+        const int y = (int)(r / W), x = (int)(r - (long long)y * W);
+        const float t = tt == TGT_U8 ? (float)static_cast<const uint8_t*>(tgt)[i] : static_cast<const float*>(tgt)[i];
+        out[b * holo + rz::b2_index(y, x, H)] = t;
     }
 }
 __global__ void __launch_bounds__(kGT) k_phase(const double2* A, float* phase, long long n) {
@@ -622,16 +636,24 @@ int mr_roots(hipStream_t st) {
 // As the float32 engine's pick: the narrow variant (half the elements per
 // thread) where the wide one would leave fewer than 4 waves per SIMD over
 // the chip, else the wide one; $SLM_RZ_PLAN=wide|narrow forces a variant.
-int rz_key(int n, long long elems) {
-    const int wide = plan_index(n, 0), narrow = plan_index(n, 1);
-    const bool w_ok = rz::key_built(wide), n_ok = rz::key_built(narrow);
-    if (!w_ok && !n_ok) return -1;
+// Column transforms take the E = 8 plan where one exists (4096: 1024-thread
+// two-column tiles at <= 128 VGPRs, 16 waves per CU where the E = 16 tiles
+// hold 8); $SLM_RZ_PLAN / $SLM_RZ_ROW_PLAN / $SLM_RZ_COL_PLAN =
+// wide|narrow|e8 force a variant (per axis for the last two).
+int rz_key(int n, long long elems, bool col) {
+    const int wide = plan_index(n, 0), narrow = plan_index(n, 1), e8 = plan_index(n, 2);
+    const bool w_ok = rz::key_built(wide), n_ok = rz::key_built(narrow), e_ok = rz::key_built(e8);
+    const char* s = std::getenv(col ? "SLM_RZ_COL_PLAN" : "SLM_RZ_ROW_PLAN");
+    if (!s) s = std::getenv("SLM_RZ_PLAN");
+    if (s) {
+        if (!std::strcmp(s, "wide") && w_ok) return wide;
+        if (!std::strcmp(s, "narrow") && n_ok) return narrow;
+        if (!std::strcmp(s, "e8") && e_ok) return e8;
+    }
+    if (col && e_ok) return e8;
+    if (!w_ok && !n_ok) return e_ok ? e8 : -1;
     if (!w_ok) return narrow;
     if (!n_ok) return wide;
-    if (const char* s = std::getenv("SLM_RZ_PLAN")) {
-        if (!std::strcmp(s, "wide")) return wide;
-        if (!std::strcmp(s, "narrow")) return narrow;
-    }
     const long long waves = elems / kPlans[wide].e / 64;
     return waves < 4LL * 1024 ? narrow : wide;
 }
@@ -648,19 +670,32 @@ int rz_cw_of(int ckey, int W) {
     return cw;
 }
 
+// State layout of the radix kernels (radix_c128.hpp LAY_RM / LAY_B2): B2 (whole
+// lines on the column side, 64-B pieces on the row side) except GS plans with a
+// 4096-point side, whose row-major rows measured faster than B2 row pairs by
+// more than the B2 columns gained (profiles/r06); $SLM_RZ_LAYOUT=rm|b2 forces one.
+int rz_layout(int algo, int H, int W) {
+    if (const char* e = std::getenv("SLM_RZ_LAYOUT")) {
+        if (!std::strcmp(e, "rm")) return rz::LAY_RM;
+        if (!std::strcmp(e, "b2")) return rz::LAY_B2;
+    }
+    return (algo == SLM_ALGO_GS && std::max(H, W) >= 4096) ? rz::LAY_RM : rz::LAY_B2;
+}
+
 struct RzChoice {
-    int rkey = -1, ckey = -1, cw = 0;
+    int rkey = -1, ckey = -1, cw = 0, lay = 0;
 };
-bool rz_shape(int B, int H, int W, RzChoice* c) {
+bool rz_shape(int B, int H, int W, RzChoice* c, int algo = SLM_ALGO_GS) {
     const char* e = std::getenv("SLM_GENERIC_ENGINE");
     if (e && (!std::strcmp(e, "mr") || !std::strcmp(e, "gemm") || !std::strcmp(e, "bluestein"))) return false;
     const long long elems = (long long)B * H * W;
-    c->rkey = rz_key(W, elems);
-    c->ckey = rz_key(H, elems);
+    c->rkey = rz_key(W, elems, false);
+    c->ckey = rz_key(H, elems, true);
     if (c->rkey < 0 || c->ckey < 0) return false;
     c->cw = rz_cw_of(c->ckey, W);
-    const int rpw = rz::rz_row_rpw(c->rkey);
-    return c->cw > 0 && rpw > 0 && H % rpw == 0;
+    c->lay = rz_layout(algo, H, W);
+    const int rpw = rz::rz_row_rpw(c->rkey, c->lay);
+    return c->cw > 0 && rpw > 0 && H % rpw == 0 && W % 2 == 0;  // B2 panels (and the target copy)
 }
 
 // Stockham twiddle table of a plan key (the float32 engine's layout,
@@ -732,7 +767,9 @@ int mr_row(GenericEngine* g, const GenericView& v, int op, mr::RowArgs a, int cl
     const size_t lds = (size_t)g->rpw * v.W * sizeof(double2);
     Mark mk(v, cls);
     if (g->rz) {
-        if (rz::rz_row_launch(g->rkey, op, a, grid, v.stream))
+        // an unchecked run's iterations before the last never take the phase branch
+        if (op == mr::RO_GS && !a.checked && !a.last) op = mr::RO_GS_MID;
+        if (rz::rz_row_launch(g->rkey, g->rz_lay, op, a, grid, v.stream))
             return slm_set_error(SLM_ERR_HIP, "complex128 radix row launch failed");
         return 0;
     }
@@ -750,6 +787,7 @@ int mr_col(GenericEngine* g, const GenericView& v, int op, mr::ColArgs a, int cl
     a.nwg = g->nwg_col;
     a.holo = v.holo;
     a.tgt = v.tgt;
+    a.tgt_blk = g->tgt_blk;
     a.tt = v.tt;
     a.e_out = v.e_out;
     a.partials = v.partials;
@@ -761,7 +799,8 @@ int mr_col(GenericEngine* g, const GenericView& v, int op, mr::ColArgs a, int cl
     const size_t lds = ((size_t)v.H << g->cw_log2) * sizeof(double2);
     Mark mk(v, cls);
     if (g->rz) {
-        if (rz::rz_col_launch(g->ckey, g->rz_cw, op, a, grid, v.stream))
+        if (op == mr::CO_GD_GRAD && v.tt == TGT_U8) op = mr::CO_GD_GRAD_U8;
+        if (rz::rz_col_launch(g->ckey, g->rz_lay, g->rz_cw, op, a, grid, v.stream))
             return slm_set_error(SLM_ERR_HIP, "complex128 radix column launch failed");
         return 0;
     }
@@ -792,6 +831,8 @@ int mr_enqueue(GenericEngine* g, const GenericView& v, int loops, double tol, in
     mr::ColArgs c;
     r.checked = c.checked = checked;
     c.wa = wa;
+    if (g->rz && g->rz_lay == rz::LAY_B2)  // the target in B2 (set_target may have changed it)
+        hipLaunchKernelGGL(k_tgt_b2, dim3(grid), dim3(kGT), 0, st, v.tgt, v.tt, g->tgt_blk, v.H, v.W, n);
     if (v.ain)  // the row passes read a_in in their digit-reversed order
         hipLaunchKernelGGL(k_ain_rev, dim3(grid_of(v.holo)), dim3(kGT), 0, st, v.ain, g->ain_rev, g->pw.rev, v.W,
                            v.holo);
@@ -886,6 +927,7 @@ void generic_destroy(GenericEngine* g) {
     for (void* p : g->tables)
         if (p) (void)hipFree(p);
     if (g->ain_rev) (void)hipFree(g->ain_rev);
+    if (g->tgt_blk) (void)hipFree(g->tgt_blk);
     delete g;
 }
 
@@ -901,16 +943,18 @@ int generic_create(const GenericView& v, GenericEngine** out) {
         return hipMalloc((void**)p, count * sizeof(double2)) == hipSuccess;
     };
     RzChoice rc;
-    if (rz_shape(v.B, v.H, v.W, &rc)) {  // complex128 radix plans: the mixed-radix buffers, Stockham tables
+    if (rz_shape(v.B, v.H, v.W, &rc, v.algo)) {  // complex128 radix plans: the mixed-radix buffers, Stockham tables
         g->mr = g->rz = true;
         g->rkey = rc.rkey;
         g->ckey = rc.ckey;
         g->rz_cw = rc.cw;
+        g->rz_lay = rc.lay;
         g->nwg_col = v.W / rc.cw;
-        g->rpw = rz::rz_row_rpw(rc.rkey);
+        g->rpw = rz::rz_row_rpw(rc.rkey, rc.lay);
         if (g->nwg_col != v.nwg) return fail_free(slm_set_error(SLM_ERR_STATE, "radix c128: partial-slab mismatch"));
         if (!alloc(&g->a, n) || !alloc(&g->b, n) || (v.algo == SLM_ALGO_GD && !alloc(&g->x, n)) ||
-            (v.has_ain && hipMalloc((void**)&g->ain_rev, (size_t)v.holo * sizeof(float)) != hipSuccess))
+            (v.has_ain && hipMalloc((void**)&g->ain_rev, (size_t)v.holo * sizeof(float)) != hipSuccess) ||
+            hipMalloc((void**)&g->tgt_blk, n * sizeof(float)) != hipSuccess)
             return fail_free(slm_set_error(SLM_ERR_HIP, "radix c128: device allocation failed"));
         if (int e = rz_plan_line(g, rc.rkey, &g->pw, v.stream)) return fail_free(e);
         if (int e = rz_plan_line(g, rc.ckey, &g->ph, v.stream)) return fail_free(e);

@@ -318,7 +318,9 @@ enum RowOp : int {
     RO_GD_INIT = 6,    // GD host field: x = field0 (complex64) -> u -> fwd -> out
     RO_GD = 7,         // GD: in (column-inverse of G) -> inv -> g a_in / S; dEdX_complex, x -= lr dEdX
                        //   (:87-91, :179-185) -> u -> fwd -> out
-    RO_NUM = 8
+    RO_GS_MID = 8,     // RO_GS of an unchecked run's iterations before the last (no phase branch;
+                       //   complex128 radix-plan kernels only: the float64 atan2 path costs registers)
+    RO_NUM = 9
 };
 enum ColOp : int {
     CO_FWD = 0,       // in -> fwd -> out
@@ -328,7 +330,9 @@ enum ColOp : int {
                       //   -> inv -> out
     CO_GD_STATS = 4,  // in -> fwd -> F; statistics of P = |F|^2 (:85-86), output
     CO_GD_GRAD = 5,   // in -> fwd -> G = mask F (s P - T) (:80,85-88) -> inv -> out
-    CO_NUM = 6
+    CO_GD_GRAD_U8 = 6,  // CO_GD_GRAD of a uint8 target (complex128 radix-plan kernels only: the
+                        //   float64 mask of numpy's dtype rule compiled apart from the float32 one)
+    CO_NUM = 7
 };
 
 struct RowArgs {
@@ -352,6 +356,7 @@ struct ColArgs {
     const double2* in = nullptr;
     double2* out = nullptr;
     const void* tgt = nullptr;
+    const float* tgt_blk = nullptr;    // complex128 radix plans: the target as float in their B2 layout
     int tt = 0;                        // TGT_U8 / TGT_F32 (row-major, as uploaded)
     float* e_out = nullptr;
     double* partials = nullptr;        // [B][max_loops][nwg][4]

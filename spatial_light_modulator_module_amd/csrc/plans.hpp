@@ -44,8 +44,15 @@ constexpr RadixPlan kPlans[] = {
     {1024, 8, 1, 4, {8, 4, 4, 8}},
     {2048, 8, 1, 4, {8, 4, 8, 8}},
     {4096, 16, 1, 3, {16, 16, 16, 0}},
+    // complex128 radix-plan kernels only (radix_c128.hpp; variant 2 is never
+    // picked by the float32 engine): 4096 in radix-8 passes, 512 threads per
+    // line -- 8 double2 per thread leave the register file room for 16 waves
+    // per CU where the E = 16 plan holds 8
+    {4096, 8, 2, 4, {8, 8, 8, 8}},
 };
 constexpr int kNumPlans = sizeof(kPlans) / sizeof(kPlans[0]);
+// plan keys of the float32 engine (kernels_inst.hip, dispatch.hpp, Makefile LENGTHS)
+constexpr int kNumF32Plans = 14;
 
 constexpr int plan_index(int n, int variant = 0) {
     for (int i = 0; i < kNumPlans; ++i)

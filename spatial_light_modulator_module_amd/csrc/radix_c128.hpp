@@ -40,13 +40,131 @@ namespace rz {
 // would not fit the register file next to the exchange)
 __host__ __device__ constexpr bool key_built(int k) { return k >= 0 && k < kNumPlans && kPlans[k].e <= 16; }
 
-template <int K>
+// Element-wise float64 pieces of these kernels: the reference's exp(i angle z)
+// and z / |z| as z times a refined reciprocal square root (v_rsq_f64 and one
+// Newton step: within ~1 ulp of 1 / sqrt, where the mixed-radix kernels pay an
+// IEEE square root and division -- each a long float64 sequence, ~1,500 VALU
+// per wave of the 4096 column pass, profiles/r06/sq_rz4096_d.txt). A float32
+// target's amplitude is numpy's float32 square root, formed in float32 (the
+// correctly rounded TgtLoad<TGT_F32>::amp, as the float32 engine).
+__device__ __forceinline__ double rsq_nr(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    return fma(y * 0.5, fma(-x * y, y, 1.0), y);
+}
+// a exp(i angle(z)) = a z / |z|, angle(0) = 0 -> a (src/algorithms.py:30,33)
+__device__ __forceinline__ double2 unit_rz(double2 z, double a) {
+    const double n2 = z.x * z.x + z.y * z.y;
+    const bool zero = n2 == 0.0;
+    const double r = a * rsq_nr(zero ? 1.0 : n2);
+    return make_double2(zero ? a : z.x * r, zero ? 0.0 : z.y * r);
+}
+// x / |x| a (src/algorithms.py:84; |x| = 0 gives NaN as there)
+__device__ __forceinline__ double2 u_rz(double2 x, double a) {
+    const double r = a * rsq_nr(x.x * x.x + x.y * x.y);
+    return make_double2(x.x * r, x.y * r);
+}
+// target intensity T (as uploaded) and numpy's amplitude sqrt(T): float16 for
+// uint8, float32 for float32, both widened
+__device__ __forceinline__ float tgt_at(const void* tgt, int tt, long long i) {
+    return tt == TGT_U8 ? (float)static_cast<const uint8_t*>(tgt)[i] : static_cast<const float*>(tgt)[i];
+}
+__device__ __forceinline__ double amp_rz(float t, int tt) {
+    return tt == TGT_U8 ? (double)TgtLoad<TGT_U8>::amp(t) : (double)TgtLoad<TGT_F32>::amp(t);
+}
+
+// Twiddles of the complex128 kernels: per butterfly one table load, w^1 =
+// exp(-2 pi i j / (Ns R)), and its powers w^r by complex products (float64:
+// r ulp-scale errors, ~1e-15, where the R - 1 table loads per butterfly were
+// most of the kernels' vector-memory instructions -- 42 of 62 per wave of the
+// 1024-point column pass, profiles/r06/sq_rz1024_d.txt). Loads laundered
+// before every transform (TW_DIRECT_LAUNDER).
+constexpr int TW_POW = 3;
+
+}  // namespace rz
+
+template <int N, class C>
+struct Twiddles<N, C, rz::TW_POW> {
+    static constexpr bool kAlwaysLaunder = true;
+    struct alignas(2 * sizeof(Scalar<C>)) Pod {
+        Scalar<C> x, y;
+    };
+    using GlobalPtr = const __attribute__((address_space(1))) Pod*;
+    GlobalPtr table;
+    __device__ __forceinline__ void launder() {
+        unsigned long long q = (unsigned long long)table;
+        asm volatile("" : "+s"(q));
+        table = (GlobalPtr)q;
+    }
+    template <int TwOff, int RegOff, int PowOff, int R, int Ns, bool INV>
+    __device__ __forceinline__ void apply(C* u, int, int j) const {
+        const C w1 = mk<C>(table[TwOff + j].x, table[TwOff + j].y);  // entry (r - 1) Ns + j at r = 1
+        C w = w1;
+        static_for<R - 1>([&](auto rc) {
+            constexpr int r = decltype(rc)::value + 1;
+            if constexpr (r > 1) w = cmul(w, w1);
+            u[r] = INV ? cmulc(u[r], w) : cmul(u[r], w);
+        });
+    }
+};
+
+namespace rz {
+
+// State layouts between the passes (template parameter LAY of both kernels):
+//  LAY_RM -- row-major both ways: the row pass moves whole lines, the column
+//    pass 32-B pieces of rows 64 KB apart (a wave-instruction load touches 32
+//    lines a quarter each);
+//  LAY_B2 -- "B2" both ways: 2-column panels, element (y, x) of a hologram at
+//    ((x / 2) H + y) 2 + x % 2. A column tile's panel is one contiguous run (a
+//    wave instruction moves 1 KB of consecutive rows, 8 whole lines); rows go
+//    in pairs (y, y + 1), y even, lanes 4k .. 4k + 3 holding (y, 2k),
+//    (y, 2k + 1), (y + 1, 2k), (y + 1, 2k + 1) of a slot: one 64-B piece of a
+//    panel per four lanes.
+// Measured per 4096^2 GS iteration (profiles/r06, one hologram): LAY_RM col
+// 289 + row 125 us, LAY_B2 col 198 + row 250 us (row pairs: one 512-thread
+// workgroup per CU), rows reading row-major and writing B2 col 318 + row 245
+// us (writes in pieces cost as much as reads). GD and 1024^2 run faster on
+// LAY_B2 (GD 1024^2 45.6 -> 40.3 us), GS 4096^2 on LAY_RM: the engine picks
+// per plan (generic.hip, rz_layout). Either way the column passes read the
+// target from a float copy in B2 made at each run's start (contiguous, where
+// the uploaded row-major target gave 8 B per row), and user arrays (phases,
+// a_in, the expected output, the GD field, the lone transforms' inputs and
+// outputs) stay row-major.
+constexpr int LAY_RM = 0, LAY_B2 = 1;
+__host__ __device__ __forceinline__ long long b2_index(long long y, int x, int H) {
+    return (((long long)(x >> 1) * H + y) << 1) + (x & 1);
+}
+
+// Row regions of a LAY_B2 pair's two rows: the second row's slots XOR 4 inside
+// each 16-slot block (a bijection), so the pair-interleaved lanes of a
+// ds_write_b128 group (8 contiguous lanes, banks (a/4) mod 32) and of a
+// ds_read_b128 group (lanes {0-3, 12-15, 20-27}, (a/4) mod 64) take
+// complementary bank halves (6 extra LDS cycles per instruction measured with
+// a plain row offset; 0 modelled for the E = 16 plans, tools/rz_lds_banks.py).
+template <bool WAVE>
+struct LdsPairRow : LdsLine<double2, 0, WAVE> {
+    int x = 0;  // 4 for the pair's second row
+    template <class C>
+    __device__ __forceinline__ void store(int l, int o, C v) const {
+        this->base[this->cur + l * this->stride + (lds_slot(o) ^ x)] = mk<double2>(v.x, v.y);
+    }
+    template <class C>
+    __device__ __forceinline__ C load(int l, int o) const {
+        const double2 v = this->base[this->cur + l * this->stride + (lds_slot(o) ^ x)];
+        return mk<C>(v.x, v.y);
+    }
+};
+
+template <int K, int LAY>
 struct RowGeo {
     static constexpr int T = PlanOf<K>::T;
-    static constexpr int RPW = T >= 256 ? 1 : 256 / T;
+    static constexpr bool PAIRS = LAY == LAY_B2;
+    static constexpr int RPW = PAIRS ? (T >= 128 ? 2 : 256 / T) : (T >= 256 ? 1 : 256 / T);
     static constexpr int THREADS = RPW * T;
-    static constexpr bool WAVE = T <= 64;  // each row inside one wave: exchanges need no barrier
+    static constexpr bool WAVE = (PAIRS ? 2 * T : T) <= 64;  // each row (pair) inside one wave: no barrier
     static constexpr int LINE = PlanOf<K>::ROWSTRIDE;
+    // 512 (row-major) / 1024 (pairs) threads, the 4096 E = 8 rows: a register
+    // budget of 16 waves per CU (<= 128 VGPRs)
+    static constexpr int MIN_WAVES = THREADS == (PAIRS ? 1024 : 512) ? 4 : 1;
 };
 
 template <int K, int CW>
@@ -58,26 +176,43 @@ struct ColGeo {
     static constexpr bool kValid = THREADS >= 64 && THREADS <= 1024 && SLOTS * 16 <= 160 * 1024;
 };
 
-template <int K, int OP>
-__global__ void __launch_bounds__((RowGeo<K>::THREADS), 1) rz_row_kernel(mr::RowArgs a) {
+template <int K, int OP, int LAY>
+__global__ void __launch_bounds__((RowGeo<K, LAY>::THREADS), (RowGeo<K, LAY>::MIN_WAVES)) rz_row_kernel(mr::RowArgs a) {
     using C = double2;
     using namespace mr;
     constexpr int N = PlanOf<K>::N, E = PlanOf<K>::E, T = PlanOf<K>::T;
-    constexpr int RPW = RowGeo<K>::RPW, LINE = RowGeo<K>::LINE;
-    constexpr bool WV = RowGeo<K>::WAVE;
+    constexpr int RPW = RowGeo<K, LAY>::RPW, LINE = RowGeo<K, LAY>::LINE;
+    constexpr bool WV = RowGeo<K, LAY>::WAVE;
     __shared__ double2 smem[RPW * LINE];
-    const int t = threadIdx.x % T, lrow = threadIdx.x / T;
+    // lane -> (row of the tile, t); LAY_B2 pairs: lanes 4k .. 4k + 3 = (r, 2k), (r, 2k + 1),
+    // (r + 1, 2k), (r + 1, 2k + 1) -- one 64-B piece of a panel per four lanes and slot
+    int t, lrow;
+    if constexpr (LAY == LAY_B2) {
+        const int q = threadIdx.x % (2 * T);
+        t = ((q >> 2) << 1) | (q & 1);
+        lrow = 2 * (threadIdx.x / (2 * T)) + ((q >> 1) & 1);
+    } else {
+        t = threadIdx.x % T;
+        lrow = threadIdx.x / T;
+    }
     const int tiles = a.H / RPW;
     const int id = xcd_remap(blockIdx.x, gridDim.x);  // neighbouring row groups on one XCD
     const int b = id / tiles;
-    const long long pix0 = (long long)((id - b * tiles) * RPW + lrow) * N;  // row start within the hologram
+    const int row = (id - b * tiles) * RPW + lrow;
+    const long long pix0 = (long long)row * N;  // row start within the hologram (row-major arrays)
     const long long off = (long long)b * a.holo + pix0;
-    if constexpr (OP == RO_GS || OP == RO_GD) {
+    const long long hoff = (long long)b * a.holo;
+    // the state: B2, or row-major
+    auto st_at = [&](int m) { return LAY == LAY_B2 ? hoff + b2_index(row, t + T * m, a.H) : off + t + T * m; };
+    if constexpr (OP == RO_GS || OP == RO_GD || OP == RO_GS_MID) {
         if (a.checked && a.iter > a.stop[b]) return;  // stopped earlier: frozen (src/algorithms.py:29,83)
     }
-    const LdsLine<double2, 0, WV> lds{smem + lrow * LINE, LINE};
-    Twiddles<K, C, TW_DIRECT> tw;
-    load_twiddles<K, C>(tw, t, a.pl.tw);
+    LdsPairRow<WV> lds;
+    lds.base = smem + lrow * LINE;
+    lds.stride = LINE;
+    lds.x = LAY == LAY_B2 ? (lrow & 1) << 2 : 0;
+    Twiddles<K, C, TW_POW> tw;
+    tw.table = (typename Twiddles<K, C, TW_POW>::GlobalPtr)a.pl.tw;
     auto ain = [&](int m) -> double { return a.ain ? (double)a.ain[pix0 + t + T * m] : 1.0; };
     C v[1][E];
 #pragma unroll
@@ -93,9 +228,11 @@ __global__ void __launch_bounds__((RowGeo<K>::THREADS), 1) rz_row_kernel(mr::Row
             const float2 f = a.field0[i];
             const double2 x = make_double2((double)f.x, (double)f.y);
             a.x[i] = x;
-            v[0][m] = u_of(x, ain(m));
+            v[0][m] = u_rz(x, ain(m));
+        } else if constexpr (OP == RO_FWD || OP == RO_INV) {
+            v[0][m] = a.in[i];  // lone transforms: row-major input
         } else {
-            v[0][m] = a.in[i];
+            v[0][m] = a.in[st_at(m)];
         }
     }
     if constexpr (OP == RO_FWD || OP == RO_WARM || OP == RO_GD_INIT) {
@@ -104,7 +241,7 @@ __global__ void __launch_bounds__((RowGeo<K>::THREADS), 1) rz_row_kernel(mr::Row
         fft_line<K, true, C>(v, t, tw, lds);
     } else if constexpr (OP == RO_COLD) {
         // A0 = ifft2(sqrt T) is complex64 (src/algorithms.py:27); B = a_in A0/|A0| (:30)
-        fft_pair<K, true, false, C>(v, t, tw, lds, [&](int, int m, C& z) { z = unit_of(round_c64(z), ain(m)); });
+        fft_pair<K, true, false, C>(v, t, tw, lds, [&](int, int m, C& z) { z = unit_rz(round_c64(z), ain(m)); });
     } else if constexpr (OP == RO_GS) {
         if (a.last || (a.checked && a.stop[b] == a.iter)) {  // uniform per workgroup
             fft_line_epi<K, true, C>(v, t, tw, lds, [&](int, int m, C& z) {
@@ -112,7 +249,9 @@ __global__ void __launch_bounds__((RowGeo<K>::THREADS), 1) rz_row_kernel(mr::Row
             });
             return;
         }
-        fft_pair<K, true, false, C>(v, t, tw, lds, [&](int, int m, C& z) { z = unit_of(z, ain(m)); });
+        fft_pair<K, true, false, C>(v, t, tw, lds, [&](int, int m, C& z) { z = unit_rz(z, ain(m)); });
+    } else if constexpr (OP == RO_GS_MID) {
+        fft_pair<K, true, false, C>(v, t, tw, lds, [&](int, int m, C& z) { z = unit_rz(z, ain(m)); });
     } else if constexpr (OP == RO_GD_FOURIER) {
         // angle of the complex64 ifft2 is float32, exp of it complex64 (:153-156)
         fft_pair<K, true, false, C>(v, t, tw, lds, [&](int, int m, C& z) {
@@ -123,7 +262,7 @@ __global__ void __launch_bounds__((RowGeo<K>::THREADS), 1) rz_row_kernel(mr::Row
             const double am = ain(m);
             const double2 x = make_double2((double)(float)co * am, (double)(float)s * am);
             a.x[off + t + T * m] = x;
-            z = u_of(x, am);
+            z = u_rz(x, am);
         });
     } else if constexpr (OP == RO_GD) {
         // dEdF = ifft2(G) a_in (unscaled transform * 1/S), dEdX_complex, x -= lr dEdX
@@ -135,11 +274,12 @@ __global__ void __launch_bounds__((RowGeo<K>::THREADS), 1) rz_row_kernel(mr::Row
             const double gx = z.x * s, gy = z.y * s;
             const long long i = off + t + T * m;
             double2 x = a.x[i];
-            const double ax2 = x.x * x.x + x.y * x.y;
-            const double ax = sqrt(ax2);
+            // dEdX_complex = (g - x Re(conj(x) g) / |x|^2) / |x| (:179-185)
+            const double inv = rsq_nr(x.x * x.x + x.y * x.y);
+            const double inv3 = inv * inv * inv;
             const double re = x.x * gx + x.y * gy;
-            x.x -= l * ((gx - x.x * (re / ax2)) / ax);
-            x.y -= l * ((gy - x.y * (re / ax2)) / ax);
+            x.x -= l * (gx * inv - x.x * re * inv3);
+            x.y -= l * (gy * inv - x.y * re * inv3);
             a.x[i] = x;
             return x;
         };
@@ -147,13 +287,13 @@ __global__ void __launch_bounds__((RowGeo<K>::THREADS), 1) rz_row_kernel(mr::Row
             fft_line_epi<K, true, C>(v, t, tw, lds, [&](int, int m, C& z) { (void)update(m, z); });
             return;
         }
-        fft_pair<K, true, false, C>(v, t, tw, lds, [&](int, int m, C& z) { z = u_of(update(m, z), ain(m)); });
+        fft_pair<K, true, false, C>(v, t, tw, lds, [&](int, int m, C& z) { z = u_rz(update(m, z), ain(m)); });
     }
 #pragma unroll
-    for (int m = 0; m < E; ++m) a.out[off + t + T * m] = v[0][m];
+    for (int m = 0; m < E; ++m) a.out[st_at(m)] = v[0][m];
 }
 
-template <int K, int CW, int OP>
+template <int K, int CW, int OP, int LAY>
 __global__ void __launch_bounds__((ColGeo<K, CW>::THREADS), 1) rz_col_kernel(mr::ColArgs a) {
     using C = double2;
     using namespace mr;
@@ -165,21 +305,30 @@ __global__ void __launch_bounds__((ColGeo<K, CW>::THREADS), 1) rz_col_kernel(mr:
     const int id = xcd_remap(blockIdx.x, gridDim.x);  // neighbouring tiles (partial lines) on one XCD
     const int b = id / a.nwg;
     const int tile = id - b * a.nwg;
-    const long long base = (long long)b * a.holo + (long long)t * a.W + tile * CW + c;  // row t, this column
-    const long long rstep = (long long)T * a.W;                                        // slot m: + m rstep
-    if constexpr (OP == CO_GS || OP == CO_GD_STATS || OP == CO_GD_GRAD) {
+    const int col = tile * CW + c;
+    const long long hoff = (long long)b * a.holo;
+    const long long base = hoff + (long long)t * a.W + col;  // row-major: row t, this column
+    const long long rstep = (long long)T * a.W;              // slot m: + m rstep
+    const long long bbase = hoff + b2_index(t, col, a.H);    // B2 (target copy, LAY_B2 state): slot m: + 2 T m
+    auto st_at = [&](int m) { return LAY == LAY_B2 ? bbase + 2LL * T * m : base + m * rstep; };
+    // the target: the B2 float copy (LAY_B2), else as uploaded (row-major; on LAY_RM the
+    // copy measured slower, 4096^2 column pass 289 -> 325 us, profiles/r06)
+    auto tgt_val = [&](int m, int tt) -> float {
+        return LAY == LAY_B2 ? a.tgt_blk[bbase + 2LL * T * m] : tgt_at(a.tgt, tt, base + m * rstep);
+    };
+    if constexpr (OP == CO_GS || OP == CO_GD_STATS || OP == CO_GD_GRAD || OP == CO_GD_GRAD_U8) {
         if (a.checked && a.iter > a.stop[b]) return;  // stopped earlier: frozen
     }
     const LdsTile<CW, double2, 0, WV> lds{smem, c};
-    Twiddles<K, C, TW_DIRECT> tw;
-    load_twiddles<K, C>(tw, t, a.pl.tw);
+    Twiddles<K, C, TW_POW> tw;
+    tw.table = (typename Twiddles<K, C, TW_POW>::GlobalPtr)a.pl.tw;
     C v[1][E];
 #pragma unroll
     for (int m = 0; m < E; ++m) {
         if constexpr (OP == CO_AMP_INV)
-            v[0][m] = make_double2(amp_of(a.tgt, a.tt, base + m * rstep), 0.0);
+            v[0][m] = make_double2(amp_rz(tgt_val(m, a.tt), a.tt), 0.0);
         else
-            v[0][m] = a.in[base + m * rstep];
+            v[0][m] = a.in[st_at(m)];
     }
     if constexpr (OP == CO_FWD) {
         fft_line<K, false, C>(v, t, tw, lds);
@@ -187,31 +336,34 @@ __global__ void __launch_bounds__((ColGeo<K, CW>::THREADS), 1) rz_col_kernel(mr:
         fft_line<K, true, C>(v, t, tw, lds);
     } else {
         double mx = 0.0, s2 = 0.0, st = 0.0;
-        auto stats = [&](int m, const C& z) -> double {
+        auto stats = [&](int m, const C& z, float tv) -> double {
             const long long i = base + m * rstep;
             const double en = z.x * z.x + z.y * z.y;
             mx = fmax(mx, en);
             s2 += en * en;
-            st += en * t_of(a.tgt, a.tt, i);
+            st += en * (double)tv;
             if (a.write_e) a.e_out[i] = (float)en;
             return en;
         };
         if constexpr (OP == CO_GS) {
             // E = |C|^2 statistics and expected output, D = a_T C/|C| (:33,36-38)
             fft_pair<K, false, true, C>(v, t, tw, lds, [&](int, int m, C& z) {
-                (void)stats(m, z);
-                z = unit_of(z, amp_of(a.tgt, a.tt, base + m * rstep));
+                const float tv = tgt_val(m, a.tt);
+                (void)stats(m, z, tv);
+                z = unit_rz(z, amp_rz(tv, a.tt));
             });
         } else if constexpr (OP == CO_GD_STATS) {
-            fft_line_epi<K, false, C>(v, t, tw, lds, [&](int, int m, C& z) { (void)stats(m, z); });
-        } else if constexpr (OP == CO_GD_GRAD) {
+            fft_line_epi<K, false, C>(v, t, tw, lds,
+                                      [&](int, int m, C& z) { (void)stats(m, z, tgt_val(m, a.tt)); });
+        } else if constexpr (OP == CO_GD_GRAD || OP == CO_GD_GRAD_U8) {
             // G = mask F (s P - T), s = norm / max P (:80,85-88); numpy's mask dtype:
             // float32 for a float32 target, float64 for uint8
             const double s = a.norm[b] / a.stats[((long long)b * a.max_loops + a.iter) * 4];
             fft_pair<K, false, true, C>(v, t, tw, lds, [&](int, int m, C& z) {
-                const double tv = t_of(a.tgt, a.tt, base + m * rstep);
-                const double mask = a.tt == TGT_U8 ? 1.0 + (double)a.wa * tv / 255.0
-                                                   : (double)(1.0f + __fdiv_rn(__fmul_rn(a.wa, (float)tv), 255.0f));
+                const double tv = (double)tgt_val(m, OP == CO_GD_GRAD_U8 ? TGT_U8 : TGT_F32);
+                const double mask = OP == CO_GD_GRAD_U8
+                                        ? 1.0 + (double)a.wa * tv / 255.0
+                                        : (double)(1.0f + __fdiv_rn(__fmul_rn(a.wa, (float)tv), 255.0f));
                 const double w = mask * ((z.x * z.x + z.y * z.y) * s - tv);
                 z = make_double2(z.x * w, z.y * w);
             });
@@ -229,16 +381,21 @@ __global__ void __launch_bounds__((ColGeo<K, CW>::THREADS), 1) rz_col_kernel(mr:
         if constexpr (OP == CO_GD_STATS) return;
     }
 #pragma unroll
-    for (int m = 0; m < E; ++m) a.out[base + m * rstep] = v[0][m];
+    for (int m = 0; m < E; ++m) {
+        if constexpr (OP == CO_FWD || OP == CO_INV)
+            a.out[base + m * rstep] = v[0][m];  // lone transforms: row-major output
+        else
+            a.out[st_at(m)] = v[0][m];
+    }
 }
 
 // ------------------------------------------------------------------------
 // host side (rz_inst.hip, one object per plan key)
 // ------------------------------------------------------------------------
-#define SLM_RZ_DECLARE(N)                                                                      \
-    int rz_row_launch_##N(int op, const mr::RowArgs& a, int grid, hipStream_t st);             \
-    int rz_col_launch_##N(int cw, int op, const mr::ColArgs& a, int grid, hipStream_t st);     \
-    int rz_row_rpw_##N();                                                                      \
+#define SLM_RZ_DECLARE(N)                                                                          \
+    int rz_row_launch_##N(int lay, int op, const mr::RowArgs& a, int grid, hipStream_t st);        \
+    int rz_col_launch_##N(int lay, int cw, int op, const mr::ColArgs& a, int grid, hipStream_t st); \
+    int rz_row_rpw_##N(int lay);                                                                   \
     int rz_col_ok_##N(int cw);
 SLM_RZ_DECLARE(0)
 SLM_RZ_DECLARE(1)
@@ -252,26 +409,27 @@ SLM_RZ_DECLARE(10)
 SLM_RZ_DECLARE(11)
 SLM_RZ_DECLARE(12)
 SLM_RZ_DECLARE(13)
+SLM_RZ_DECLARE(14)
 #undef SLM_RZ_DECLARE
-#define SLM_RZ_FOR_EACH_KEY(X) X(0) X(1) X(2) X(3) X(5) X(6) X(8) X(9) X(10) X(11) X(12) X(13)
+#define SLM_RZ_FOR_EACH_KEY(X) X(0) X(1) X(2) X(3) X(5) X(6) X(8) X(9) X(10) X(11) X(12) X(13) X(14)
 
 // launch op on plan key k (0 on success, -1 on a launch error or an unbuilt key)
-inline int rz_row_launch(int k, int op, const mr::RowArgs& a, int grid, hipStream_t st) {
+inline int rz_row_launch(int k, int lay, int op, const mr::RowArgs& a, int grid, hipStream_t st) {
 #define SLM_CASE(N) \
-    case N: return rz_row_launch_##N(op, a, grid, st);
+    case N: return rz_row_launch_##N(lay, op, a, grid, st);
     switch (k) { SLM_RZ_FOR_EACH_KEY(SLM_CASE) default: return -1; }
 #undef SLM_CASE
 }
-inline int rz_col_launch(int k, int cw, int op, const mr::ColArgs& a, int grid, hipStream_t st) {
+inline int rz_col_launch(int k, int lay, int cw, int op, const mr::ColArgs& a, int grid, hipStream_t st) {
 #define SLM_CASE(N) \
-    case N: return rz_col_launch_##N(cw, op, a, grid, st);
+    case N: return rz_col_launch_##N(lay, cw, op, a, grid, st);
     switch (k) { SLM_RZ_FOR_EACH_KEY(SLM_CASE) default: return -1; }
 #undef SLM_CASE
 }
-// rows per row tile of key k (0: not built)
-inline int rz_row_rpw(int k) {
+// rows per row tile of key k on layout lay (0: not built)
+inline int rz_row_rpw(int k, int lay) {
 #define SLM_CASE(N) \
-    case N: return rz_row_rpw_##N();
+    case N: return rz_row_rpw_##N(lay);
     switch (k) { SLM_RZ_FOR_EACH_KEY(SLM_CASE) default: return 0; }
 #undef SLM_CASE
 }

@@ -79,11 +79,14 @@ def test_rz_gs_warm_start_vs_oracle(gpu, f64_engine, shape, u8):
 
 
 @pytest.mark.gpu
-def test_rz_matches_mixed_radix(gpu, monkeypatch):
-    """Both complex128 back ends on one warm-started batch: the same
-    contract, transforms that round differently (~1e-16), so phases and
-    error curves agree far inside the float32 output's rounding."""
+@pytest.mark.parametrize("layout", ["rm", "b2"])
+def test_rz_matches_mixed_radix(gpu, monkeypatch, layout):
+    """Both complex128 back ends on one warm-started batch, the radix kernels on
+    each state layout (radix_c128.hpp LAY_RM / LAY_B2): the same contract,
+    transforms that round differently (~1e-16), so phases and error curves
+    agree far inside the float32 output's rounding."""
     monkeypatch.setenv("SLM_ENGINE", "float64")
+    monkeypatch.setenv("SLM_RZ_LAYOUT", layout)
     t = np.stack([_target((256, 512), False, seed=s) for s in (1, 2)])
     phi = np.random.default_rng(3).uniform(-np.pi, np.pi, t.shape).astype(np.float32)
     monkeypatch.delenv("SLM_GENERIC_ENGINE", raising=False)
@@ -91,7 +94,7 @@ def test_rz_matches_mixed_radix(gpu, monkeypatch):
     monkeypatch.setenv("SLM_GENERIC_ENGINE", "mr")
     ph_m, e_m, st_m, _ = _gs(gpu, t, 25, phi, want="mixed-radix")
     d = float(np.max(np.abs(np.angle(np.exp(1j * (ph_z.astype(np.float64) - ph_m))))))
-    print(f"[parity] radix-c128 vs mixed-radix GS 2 x 256x512, 25 iterations: max phase difference {d:.3e}")
+    print(f"[parity] radix-c128 ({layout}) vs mixed-radix GS 2 x 256x512, 25 iterations: max phase difference {d:.3e}")
     assert d < 1e-5  # float32 outputs: an angle near a rounding boundary moves by one float32 ulp
     np.testing.assert_allclose(st_z[:, :25, 3], st_m[:, :25, 3], rtol=1e-10)
     np.testing.assert_allclose(e_z, e_m, rtol=1e-6)
@@ -111,11 +114,15 @@ def _gd_run(lib, t, loops, x0):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("engine", ["radix-c128", "mixed-radix"])
+@pytest.mark.parametrize("engine", ["radix-c128", "radix-c128-rm", "mixed-radix"])
 def test_rz_gd_vs_oracle(gpu, monkeypatch, engine):
-    """GD (src/algorithms.py:60-112) on both complex128 back ends from the
+    """GD (src/algorithms.py:60-112) on both complex128 back ends (the radix
+    kernels on their default B2 layout and on the row-major one) from the
     random guess (set on the host, seed 42), against the faithful float64 oracle."""
     monkeypatch.setenv("SLM_ENGINE", "float64")
+    if engine == "radix-c128-rm":
+        monkeypatch.setenv("SLM_RZ_LAYOUT", "rm")
+        engine = "radix-c128"
     if engine == "mixed-radix":
         monkeypatch.setenv("SLM_GENERIC_ENGINE", "mr")
     else:
