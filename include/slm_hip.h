@@ -146,7 +146,9 @@ int slm_plan_layout(slm_plan* plan, int* x_log2, int* y_log2);
  * prime factor above 13), 3 = mixed radix (float64 in-place radix-2..13
  * kernels: other sides without a float32 radix plan), 4 = complex128 radix
  * plans (float64 Stockham kernels with complex128 state: 2^k / 768 sides
- * under $SLM_ENGINE=float64) */
+ * under $SLM_ENGINE=float64), 5 = complex64 radix plans (the same kernels at
+ * float32: GS on 13-smooth SLM panel sides such as 1080 x 1920, float32
+ * precision; slm_plan_set_precision(F64) moves such a plan to engine 3) */
 int slm_plan_engine(slm_plan* plan, int* col_engine, int* row_engine);
 /* HIP device the plan lives on */
 int slm_plan_device(slm_plan* plan);

@@ -352,10 +352,12 @@ class Plan:
         transforms along rows and transposed columns, Bluestein's chirp-z
         for a side with a larger prime factor, generic.hip), and under
         $SLM_ENGINE=float64 on 2^k / 768 sides "radix-c128" (float64
-        Stockham kernels with complex128 state, radix_c128.hpp)."""
+        Stockham kernels with complex128 state, radix_c128.hpp); float32 GS on
+        13-smooth SLM panel sides (e.g. 1080 x 1920) "radix-c64" (the same
+        kernels with complex64 state and float32 butterflies)."""
         c, r = ctypes.c_int(), ctypes.c_int()
         check(self._lib.slm_plan_engine(self.handle, ctypes.byref(c), ctypes.byref(r)), "slm_plan_engine")
-        names = ("stockham", "shuffle", "bluestein", "mixed-radix", "radix-c128")
+        names = ("stockham", "shuffle", "bluestein", "mixed-radix", "radix-c128", "radix-c64")
         return names[c.value], names[r.value]
 
     def layout(self) -> tuple[int, int]:

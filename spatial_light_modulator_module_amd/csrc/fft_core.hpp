@@ -591,6 +591,14 @@ template <int N, int E, int L, bool INV, int Ns, int TwOff, int RegOff, int PowO
           class Tw, class Sink, int R, int... Rest>
 __device__ __forceinline__ void stockham_from(V (&v)[L][E], int t, const Tw& tw, const Lds& lds, Sink& sink) {
     constexpr int T = N / E;
+    // The LDS slots and twiddle indices of a pass are functions of t alone, so
+    // the compiler computes every pass's (and both transforms' of a pair) up
+    // front and keeps them live: 386 registers for the 1920-point complex64
+    // row pair, 149 with t passed through an empty asm per pass (each pass
+    // then recomputes its own). The any-size engine's radix kernels
+    // (kAlwaysLaunder twiddle modes) take it; the float32 engine keeps its
+    // measured schedule.
+    if constexpr (Tw::kAlwaysLaunder) asm volatile("" : "+v"(t));
     constexpr int NB = E / R;
     static_assert(E % R == 0, "radix must divide elements per thread");
     static_for<NB>([&](auto kc) {

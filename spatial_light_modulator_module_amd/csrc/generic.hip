@@ -2,11 +2,13 @@
 // float32 radix plan covers, in complex float64 like the reference's loop.
 //
 // Three transform back ends:
-//  * complex128 radix plans (radix_c128.hpp; the default where both sides
-//    have a radix plan, plans.hpp: 2^k and 768 -- reached through
-//    $SLM_ENGINE=float64): the mixed-radix launch structure and contract on
-//    compile-time Stockham transforms with the line in registers and
-//    complex128 LDS exchanges;
+//  * radix plans (radix_c128.hpp; the default where both sides have a radix
+//    plan, plans.hpp): the mixed-radix launch structure and contract on
+//    compile-time Stockham transforms with the line in registers and LDS
+//    exchanges. Complex128 on 2^k and 768 sides (reached through
+//    $SLM_ENGINE=float64); complex64 for GS at float32 precision where a side
+//    is a 13-smooth SLM panel length (600 .. 1920, plans.hpp variant 3) --
+//    e.g. 1080 x 1920 -- the float32 engine's numerics on these shapes;
 //  * mixed radix (mixed_radix.hpp, mr_inst.hip; the default wherever both
 //    sides factor into 2, 3, 5, 7, 11, 13 and fit a workgroup's LDS): the
 //    iteration is two fused launches -- column pass (forward transform,
@@ -51,6 +53,7 @@ struct GenericEngine {
     int rkey = -1, ckey = -1;  // plan keys (plans.hpp) of the row / column transforms
     int rz_cw = 0;             // columns per column tile
     int rz_lay = 0;            // state layout between the passes (radix_c128.hpp LAY_RM / LAY_B2)
+    int prec = PREC_F64;       // PREC_F32: complex64 radix kernels (the state buffers then hold float2)
     float* tgt_blk = nullptr;  // the target as float in the radix kernels' B2 layout (rebuilt per run)
     bool big = false;        // a radix outside mr::small_radix in either plan (7, 11, 13)
     mr::LinePlan pw, ph;     // row (length W) and column (length H) transforms
@@ -199,6 +202,18 @@ __global__ void __launch_bounds__(kGT) k_phase_exp(const float* phase, double2* 
 __global__ void __launch_bounds__(kGT) k_abs2(const double2* C, float* out, long long n) {
     for (long long i = blockIdx.x * (long long)kGT + threadIdx.x; i < n; i += (long long)gridDim.x * kGT)
         out[i] = (float)(C[i].x * C[i].x + C[i].y * C[i].y);
+}
+// complex64 engine: exp(1j phase) of a float32 phase is complex64 (numpy), |C|^2 float32
+__global__ void __launch_bounds__(kGT) k_phase_exp_c64(const float* phase, float2* B, long long n) {
+    for (long long i = blockIdx.x * (long long)kGT + threadIdx.x; i < n; i += (long long)gridDim.x * kGT) {
+        double s, c;
+        sincos((double)phase[i], &s, &c);
+        B[i] = make_float2((float)c, (float)s);
+    }
+}
+__global__ void __launch_bounds__(kGT) k_abs2_c64(const float2* C, float* out, long long n) {
+    for (long long i = blockIdx.x * (long long)kGT + threadIdx.x; i < n; i += (long long)gridDim.x * kGT)
+        out[i] = C[i].x * C[i].x + C[i].y * C[i].y;
 }
 
 // Statistics block `blockIdx.x` of hologram `blockIdx.y`: a contiguous chunk.
@@ -632,7 +647,9 @@ int mr_roots(hipStream_t st) {
 // ------------------------------------------------------------------------
 // complex128 radix-plan back end (host side)
 // ------------------------------------------------------------------------
-// Plan key of one axis: both sides need a built radix plan (rz::key_built).
+// Plan key of one axis: both sides need a built radix plan (rz::key_built) at
+// the engine's precision; a 13-smooth panel side (plans.hpp variant 3,
+// complex64 only) has its one plan.
 // As the float32 engine's pick: the narrow variant (half the elements per
 // thread) where the wide one would leave fewer than 4 waves per SIMD over
 // the chip, else the wide one; $SLM_RZ_PLAN=wide|narrow forces a variant.
@@ -640,9 +657,10 @@ int mr_roots(hipStream_t st) {
 // two-column tiles at <= 128 VGPRs, 16 waves per CU where the E = 16 tiles
 // hold 8); $SLM_RZ_PLAN / $SLM_RZ_ROW_PLAN / $SLM_RZ_COL_PLAN =
 // wide|narrow|e8 force a variant (per axis for the last two).
-int rz_key(int n, long long elems, bool col) {
-    const int wide = plan_index(n, 0), narrow = plan_index(n, 1), e8 = plan_index(n, 2);
-    const bool w_ok = rz::key_built(wide), n_ok = rz::key_built(narrow), e_ok = rz::key_built(e8);
+int rz_key(int n, long long elems, bool col, int prec) {
+    const int wide = plan_index(n, 0), narrow = plan_index(n, 1), e8 = plan_index(n, 2), panel = plan_index(n, 3);
+    if (rz::key_built(panel, prec)) return panel;
+    const bool w_ok = rz::key_built(wide, prec), n_ok = rz::key_built(narrow, prec), e_ok = rz::key_built(e8, prec);
     const char* s = std::getenv(col ? "SLM_RZ_COL_PLAN" : "SLM_RZ_ROW_PLAN");
     if (!s) s = std::getenv("SLM_RZ_PLAN");
     if (s) {
@@ -662,11 +680,11 @@ int rz_key(int n, long long elems, bool col) {
 // workgroups per CU (4 columns of 64 threads, 2 of 128), 2 for 256-thread
 // lines (4096: one 512-thread workgroup per CU, 32-B row segments), 8 for
 // 8-thread lines; $SLM_RZ_CW overrides.
-int rz_cw_of(int ckey, int W) {
+int rz_cw_of(int ckey, int W, int prec) {
     const int T = kPlans[ckey].n / kPlans[ckey].e;
     int cw = T >= 128 ? 2 : T >= 16 ? 4 : 8;
     if (const char* e = std::getenv("SLM_RZ_CW")) cw = std::atoi(e);
-    if (cw < 1 || W % cw || !rz::rz_col_ok(ckey, cw)) return 0;
+    if (cw < 1 || W % cw || !rz::rz_col_ok(ckey, prec, cw)) return 0;
     return cw;
 }
 
@@ -674,7 +692,9 @@ int rz_cw_of(int ckey, int W) {
 // lines on the column side, 64-B pieces on the row side) except GS plans with a
 // 4096-point side, whose row-major rows measured faster than B2 row pairs by
 // more than the B2 columns gained (profiles/r06); $SLM_RZ_LAYOUT=rm|b2 forces one.
-int rz_layout(int algo, int H, int W) {
+// The complex64 kernels are built on B2 only.
+int rz_layout(int algo, int H, int W, int prec) {
+    if (prec == PREC_F32) return rz::LAY_B2;
     if (const char* e = std::getenv("SLM_RZ_LAYOUT")) {
         if (!std::strcmp(e, "rm")) return rz::LAY_RM;
         if (!std::strcmp(e, "b2")) return rz::LAY_B2;
@@ -685,22 +705,26 @@ int rz_layout(int algo, int H, int W) {
 struct RzChoice {
     int rkey = -1, ckey = -1, cw = 0, lay = 0;
 };
-bool rz_shape(int B, int H, int W, RzChoice* c, int algo = SLM_ALGO_GS) {
+// complex64 radix kernels: GS only (GD's 500-iteration gradient loop keeps
+// complex128 state)
+bool rz_shape(int B, int H, int W, RzChoice* c, int algo, int prec) {
     const char* e = std::getenv("SLM_GENERIC_ENGINE");
     if (e && (!std::strcmp(e, "mr") || !std::strcmp(e, "gemm") || !std::strcmp(e, "bluestein"))) return false;
+    if (prec == PREC_F32 && algo != SLM_ALGO_GS) return false;
     const long long elems = (long long)B * H * W;
-    c->rkey = rz_key(W, elems, false);
-    c->ckey = rz_key(H, elems, true);
+    c->rkey = rz_key(W, elems, false, prec);
+    c->ckey = rz_key(H, elems, true, prec);
     if (c->rkey < 0 || c->ckey < 0) return false;
-    c->cw = rz_cw_of(c->ckey, W);
-    c->lay = rz_layout(algo, H, W);
+    c->cw = rz_cw_of(c->ckey, W, prec);
+    c->lay = rz_layout(algo, H, W, prec);
     const int rpw = rz::rz_row_rpw(c->rkey, c->lay);
     return c->cw > 0 && rpw > 0 && H % rpw == 0 && W % 2 == 0;  // B2 panels (and the target copy)
 }
 
 // Stockham twiddle table of a plan key (the float32 engine's layout,
 // slm_capi.hip get_twiddles: every pass after the first holds (R - 1) Ns
-// entries exp(-2 pi i j r / (Ns R))) and the identity order (natural in and out)
+// entries exp(-2 pi i j r / (Ns R)); float2 for the complex64 kernels) and the
+// identity order (natural in and out)
 int rz_plan_line(GenericEngine* g, int key, mr::LinePlan* pl, hipStream_t st) {
     const RadixPlan& rp = kPlans[key];
     std::vector<double> tw;
@@ -725,12 +749,16 @@ int rz_plan_line(GenericEngine* g, int key, mr::LinePlan* pl, hipStream_t st) {
     }
     std::vector<int> rev(rp.n);
     for (int e = 0; e < rp.n; ++e) rev[e] = e;
+    std::vector<float> twf(tw.begin(), tw.end());
+    const bool f32 = g->prec == PREC_F32;
+    const size_t tw_bytes = f32 ? twf.size() * sizeof(float) : tw.size() * sizeof(double);
     void *dtw = nullptr, *drev = nullptr;
-    if (hipMalloc(&dtw, tw.size() * sizeof(double)) != hipSuccess) return slm_set_error(SLM_ERR_HIP, "radix c128: allocation");
+    if (hipMalloc(&dtw, tw_bytes) != hipSuccess) return slm_set_error(SLM_ERR_HIP, "radix plans: allocation");
     g->tables.push_back(dtw);
-    if (hipMalloc(&drev, rev.size() * sizeof(int)) != hipSuccess) return slm_set_error(SLM_ERR_HIP, "radix c128: allocation");
+    if (hipMalloc(&drev, rev.size() * sizeof(int)) != hipSuccess) return slm_set_error(SLM_ERR_HIP, "radix plans: allocation");
     g->tables.push_back(drev);
-    G_HIP(hipMemcpyAsync(dtw, tw.data(), tw.size() * sizeof(double), hipMemcpyHostToDevice, st));
+    G_HIP(hipMemcpyAsync(dtw, f32 ? (const void*)twf.data() : (const void*)tw.data(), tw_bytes, hipMemcpyHostToDevice,
+                         st));
     G_HIP(hipMemcpyAsync(drev, rev.data(), rev.size() * sizeof(int), hipMemcpyHostToDevice, st));
     G_HIP(hipStreamSynchronize(st));
     pl->n = rp.n;
@@ -769,8 +797,8 @@ int mr_row(GenericEngine* g, const GenericView& v, int op, mr::RowArgs a, int cl
     if (g->rz) {
         // an unchecked run's iterations before the last never take the phase branch
         if (op == mr::RO_GS && !a.checked && !a.last) op = mr::RO_GS_MID;
-        if (rz::rz_row_launch(g->rkey, g->rz_lay, op, a, grid, v.stream))
-            return slm_set_error(SLM_ERR_HIP, "complex128 radix row launch failed");
+        if (rz::rz_row_launch(g->rkey, g->prec, g->rz_lay, op, a, grid, v.stream))
+            return slm_set_error(SLM_ERR_HIP, "radix-plan row launch failed");
         return 0;
     }
     if (mr::mr_row_launch(op, g->big, a, grid, lds, v.stream))
@@ -800,8 +828,8 @@ int mr_col(GenericEngine* g, const GenericView& v, int op, mr::ColArgs a, int cl
     Mark mk(v, cls);
     if (g->rz) {
         if (op == mr::CO_GD_GRAD && v.tt == TGT_U8) op = mr::CO_GD_GRAD_U8;
-        if (rz::rz_col_launch(g->ckey, g->rz_lay, g->rz_cw, op, a, grid, v.stream))
-            return slm_set_error(SLM_ERR_HIP, "complex128 radix column launch failed");
+        if (rz::rz_col_launch(g->ckey, g->prec, g->rz_lay, g->rz_cw, op, a, grid, v.stream))
+            return slm_set_error(SLM_ERR_HIP, "radix-plan column launch failed");
         return 0;
     }
     if (mr::mr_col_launch(op, g->big, a, grid, lds, v.stream))
@@ -903,9 +931,14 @@ int mr_enqueue(GenericEngine* g, const GenericView& v, int loops, double tol, in
 
 }  // namespace
 
-int generic_nwg(int B, int H, int W, long long holo) {
+int generic_precision(int B, int H, int W, int algo, int prec) {
     RzChoice rc;
-    if (rz_shape(B, H, W, &rc)) return W / rc.cw;
+    return prec == PREC_F32 && rz_shape(B, H, W, &rc, algo, PREC_F32) ? PREC_F32 : PREC_F64;
+}
+
+int generic_nwg(int B, int H, int W, long long holo, int algo, int prec) {
+    RzChoice rc;
+    if (rz_shape(B, H, W, &rc, algo, generic_precision(B, H, W, algo, prec))) return W / rc.cw;
     if (mr_shape_ok(H, W)) {
         const MrTiling t = mr_tiling(B, H, W);
         return (W + (1 << t.cw_log2) - 1) >> t.cw_log2;
@@ -918,7 +951,9 @@ bool generic_uses_blas(const GenericEngine* g) {
     return false;
 }
 
-int generic_kind(const GenericEngine* g) { return !g ? -1 : g->rz ? 4 : g->mr ? 3 : 2; }  // 2: line transforms
+int generic_kind(const GenericEngine* g) {  // 2: line transforms
+    return !g ? -1 : g->rz ? (g->prec == PREC_F32 ? 5 : 4) : g->mr ? 3 : 2;
+}
 
 void generic_destroy(GenericEngine* g) {
     if (!g) return;
@@ -943,8 +978,10 @@ int generic_create(const GenericView& v, GenericEngine** out) {
         return hipMalloc((void**)p, count * sizeof(double2)) == hipSuccess;
     };
     RzChoice rc;
-    if (rz_shape(v.B, v.H, v.W, &rc, v.algo)) {  // complex128 radix plans: the mixed-radix buffers, Stockham tables
+    const int prec = generic_precision(v.B, v.H, v.W, v.algo, v.prec);
+    if (rz_shape(v.B, v.H, v.W, &rc, v.algo, prec)) {  // radix plans: the mixed-radix buffers, Stockham tables
         g->mr = g->rz = true;
+        g->prec = prec;
         g->rkey = rc.rkey;
         g->ckey = rc.ckey;
         g->rz_cw = rc.cw;
@@ -1062,6 +1099,8 @@ int generic_field(GenericEngine* g, const GenericView& v, float2* out) {
 
 int generic_fft2(GenericEngine* g, const GenericView& v, const float2* in, float2* out, int inverse) {
     const long long n = (long long)v.B * v.holo;
+    if (g->prec == PREC_F32)  // complex64 radix kernels: straight on the caller's buffers
+        return mr_fft2(g, v, reinterpret_cast<const double2*>(in), reinterpret_cast<double2*>(out), inverse != 0);
     hipLaunchKernelGGL(k_c64_to_c128, dim3(grid_of(n)), dim3(kGT), 0, v.stream, in, g->b, n);
     if (int rc = g->mr ? mr_fft2(g, v, g->b, g->b, inverse != 0) : dft2(g, v, g->b, g->b, inverse != 0)) return rc;
     hipLaunchKernelGGL(k_c128_to_c64, dim3(grid_of(n)), dim3(kGT), 0, v.stream, g->b, out, n);
@@ -1071,6 +1110,14 @@ int generic_fft2(GenericEngine* g, const GenericView& v, const float2* in, float
 
 int generic_intensity(GenericEngine* g, const GenericView& v, const float* phase, float* out) {
     const long long n = (long long)v.B * v.holo;
+    if (g->prec == PREC_F32) {
+        float2* b = reinterpret_cast<float2*>(g->b);
+        hipLaunchKernelGGL(k_phase_exp_c64, dim3(grid_of(n)), dim3(kGT), 0, v.stream, phase, b, n);
+        if (int rc = mr_fft2(g, v, g->b, g->b, false)) return rc;
+        hipLaunchKernelGGL(k_abs2_c64, dim3(grid_of(n)), dim3(kGT), 0, v.stream, b, out, n);
+        G_HIP(hipGetLastError());
+        return 0;
+    }
     hipLaunchKernelGGL(k_phase_exp, dim3(grid_of(n)), dim3(kGT), 0, v.stream, phase, g->b, n);
     if (int rc = g->mr ? mr_fft2(g, v, g->b, g->b, false) : dft2(g, v, g->b, g->b, false)) return rc;
     hipLaunchKernelGGL(k_abs2, dim3(grid_of(n)), dim3(kGT), 0, v.stream, g->b, out, n);
@@ -1079,6 +1126,7 @@ int generic_intensity(GenericEngine* g, const GenericView& v, const float* phase
 }
 
 int generic_fft2_z(GenericEngine* g, const GenericView& v, const double2* in, double2* out, int inverse) {
+    if (g->prec != PREC_F64) return slm_set_error(SLM_ERR_STATE, "fft2_c128 on a complex64 engine");
     return g->mr ? mr_fft2(g, v, in, out, inverse != 0) : dft2(g, v, in, out, inverse != 0);
 }
 

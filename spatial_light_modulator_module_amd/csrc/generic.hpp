@@ -2,7 +2,8 @@
 // (plans.hpp) covers. The reference takes any (h, w) (src/algorithms.py:20-27;
 // scipy.fft handles every length), so such plans run in complex float64 with
 // row-major state: on the complex128 radix-plan kernels (radix_c128.hpp) where
-// both sides have a radix plan ($SLM_ENGINE=float64), on hand-written
+// both sides have a radix plan ($SLM_ENGINE=float64; their complex64 variant
+// runs GS on 13-smooth SLM panels such as 1080 x 1920), on hand-written
 // mixed-radix transforms (mixed_radix.hpp) where both sides factor into 2, 3,
 // 5, 7, 11, 13, otherwise as 1-D line transforms (direct, or Bluestein's
 // chirp-z over a mixed-radix length) plus element-wise kernels. slm_capi.hip
@@ -17,6 +18,10 @@ struct GenericEngine;
 // the slm_plan buffers the engine reads and writes (row-major [B][H][W])
 struct GenericView {
     int algo = 0, B = 0, H = 0, W = 0, tt = 0, has_ain = 0, max_loops = 0, nwg = 0;
+    // requested arithmetic (kernels.hpp Precision): PREC_F32 takes the complex64
+    // radix kernels where both sides have one (GS only), else the engine runs
+    // in float64; generic_precision reports what it runs
+    int prec = 1;
     long long holo = 0;
     hipStream_t stream = nullptr;
     const void* tgt = nullptr;      // target intensity (uint8 or float32)
@@ -39,11 +44,14 @@ struct GenericView {
 
 // statistics blocks per hologram (the partials' nwg): column tiles of the
 // mixed-radix / radix-plan back ends, element chunks of the line-transform one
-int generic_nwg(int B, int H, int W, long long holo);
+int generic_nwg(int B, int H, int W, long long holo, int algo = 0, int prec = 1);
+// the precision a plan of this shape, algorithm and requested precision runs at
+int generic_precision(int B, int H, int W, int algo, int prec);
 // true for a back end whose runs cannot be graph-captured (none since r06,
 // when the rocBLAS DFT products gave way to the line transforms)
 bool generic_uses_blas(const GenericEngine* g);
-// back end: 2 line transforms (chirp-z), 3 mixed radix, 4 complex128 radix plans (slm_plan_engine codes)
+// back end: 2 line transforms (chirp-z), 3 mixed radix, 4 complex128 radix plans,
+// 5 complex64 radix plans (slm_plan_engine codes)
 int generic_kind(const GenericEngine* g);
 int generic_create(const GenericView& v, GenericEngine** out);
 void generic_destroy(GenericEngine* g);

@@ -515,6 +515,43 @@ __device__ __forceinline__ double wave_fold(double x) {
 // Block-wide reduction of (max, sum, sum); result valid in thread 0.
 template <int THREADS>
 __device__ __forceinline__ void block_reduce_stats(double& mx, double& s2, double& st) {
+    if constexpr (THREADS % 64 != 0) {
+        // a partial last wave (the panel plans' column tiles, e.g. 4 x 36 threads):
+        // its missing lanes hold no values, so fold inside 16-lane rows (DPP row
+        // and quad moves) -- or quads where the block is not whole rows -- and
+        // combine those through LDS
+        constexpr int G = THREADS % 16 == 0 ? 16 : 4;
+        static_assert(THREADS % 4 == 0, "partial waves of whole quads");
+        constexpr int NR = THREADS / G;
+        __shared__ double red16[NR][3];
+        auto fold = [](double x, auto op) {
+            if constexpr (G == 16) {
+                x = op(x, dpp_f64<kDppRor4>(x));
+                x = op(x, dpp_f64<kDppRor8>(x));
+            }
+            x = op(x, dpp_f64<kDppQuadXor1>(x));
+            return op(x, dpp_f64<kDppQuadXor2>(x));
+        };
+        auto fmx = [](double a, double b) { return fmax(a, b); };
+        auto add = [](double a, double b) { return a + b; };
+        mx = fold(mx, fmx);
+        s2 = fold(s2, add);
+        st = fold(st, add);
+        if (threadIdx.x % G == 0) {
+            red16[threadIdx.x / G][0] = mx;
+            red16[threadIdx.x / G][1] = s2;
+            red16[threadIdx.x / G][2] = st;
+        }
+        lds_barrier();
+        if (threadIdx.x == 0) {
+            for (int r = 1; r < NR; ++r) {
+                mx = fmax(mx, red16[r][0]);
+                s2 += red16[r][1];
+                st += red16[r][2];
+            }
+        }
+        return;
+    }
     constexpr int NW = (THREADS + 63) / 64;
     __shared__ double red[NW][3];
     mx = wave_fold<true>(mx);

@@ -16,7 +16,7 @@ struct RadixPlan {
     int e;        // complex elements held per thread
     int variant;  // 0 = wide (16-24 elements per thread), 1 = narrow (twice the threads)
     int npass;    // number of Stockham passes
-    int r[4];     // radices, first pass first
+    int r[8];     // radices, first pass first
 };
 
 // Lengths the library supports along either image axis. 768 = 3 * 256 is the
@@ -49,6 +49,20 @@ constexpr RadixPlan kPlans[] = {
     // line -- 8 double2 per thread leave the register file room for 16 waves
     // per CU where the E = 16 plan holds 8
     {4096, 8, 2, 4, {8, 8, 8, 8}},
+    // complex64 radix kernels of the any-size engine only (radix_c128.hpp at
+    // float32, variant 3): 13-smooth SLM panel sides. Every radix divides E
+    // (the Stockham slot model), so a side with the factors 3 and 5 needs a
+    // multiple of 15 elements per thread; first and last radix equal where the
+    // factors allow (fused projection, fft_pair).
+    {600, 30, 3, 3, {10, 6, 10}},
+    {800, 20, 3, 3, {20, 2, 20}},
+    {1000, 10, 3, 3, {10, 10, 10}},
+    {1080, 30, 3, 4, {6, 5, 6, 6}},
+    {1152, 24, 3, 3, {12, 8, 12}},
+    {1200, 30, 3, 4, {10, 2, 6, 10}},
+    {1280, 20, 3, 4, {4, 20, 4, 4}},
+    {1536, 24, 3, 3, {8, 24, 8}},
+    {1920, 30, 3, 7, {2, 2, 2, 30, 2, 2, 2}},
 };
 constexpr int kNumPlans = sizeof(kPlans) / sizeof(kPlans[0]);
 // plan keys of the float32 engine (kernels_inst.hip, dispatch.hpp, Makefile LENGTHS)

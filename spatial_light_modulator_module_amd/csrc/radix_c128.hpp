@@ -1,5 +1,6 @@
-// Complex128 radix-plan kernels: the any-size engine's back end for image
-// sides that have a compile-time radix plan (plans.hpp: 2^k and 768).
+// Radix-plan kernels of the any-size engine: image sides that have a
+// compile-time radix plan (plans.hpp) -- complex128 on 2^k and 768 sides,
+// complex64 (template P, below) also on the 13-smooth SLM panel sides.
 //
 // The reference's loop runs in complex128 after its first ifft2
 // (src/algorithms.py:27-38, 83-93). The float32 engine (kernels.hpp) keeps
@@ -36,9 +37,19 @@
 namespace slm {
 namespace rz {
 
-// plan keys built (plans.hpp): every plan with E <= 16 (E = 24 / 32 double2
-// would not fit the register file next to the exchange)
-__host__ __device__ constexpr bool key_built(int k) { return k >= 0 && k < kNumPlans && kPlans[k].e <= 16; }
+// Precisions of these kernels (template P): PREC_F64 -- complex128 state,
+// float64 arithmetic, complex128 exchanges ($SLM_ENGINE=float64, 2^k / 768
+// sides); PREC_F32 -- complex64 state, float32 butterflies and projections,
+// complex64 exchanges, the float32 engine's numerics (GS on 13-smooth SLM
+// panel sides by default: plans.hpp variant 3, e.g. 1080 x 1920).
+// Plan keys built per precision: float64 every plan with E <= 16 outside the
+// panel plans (E = 24 / 32 double2 would not fit the register file next to
+// the exchange); float32 every plan with E <= 30 (the panel plans need a
+// multiple of 15 elements per thread).
+__host__ __device__ constexpr bool key_built(int k, int p = PREC_F64) {
+    return k >= 0 && k < kNumPlans &&
+           (p == PREC_F64 ? kPlans[k].e <= 16 && kPlans[k].variant != 3 : kPlans[k].e <= 30);
+}
 
 // Element-wise float64 pieces of these kernels: the reference's exp(i angle z)
 // and z / |z| as z times a refined reciprocal square root (v_rsq_f64 and one
@@ -63,14 +74,26 @@ __device__ __forceinline__ double2 u_rz(double2 x, double a) {
     const double r = a * rsq_nr(x.x * x.x + x.y * x.y);
     return make_double2(x.x * r, x.y * r);
 }
+// float32 (PREC_F32) counterparts: the float32 engine's (kernels.hpp unit_scale,
+// normalize, rsqrt_nr)
+__device__ __forceinline__ float2 unit_rz(float2 z, float a) { return unit_scale(z, a); }
+__device__ __forceinline__ float2 u_rz(float2 x, float a) { return normalize(x, a); }
+__device__ __forceinline__ float rsq_nr(float x) { return rsqrt_nr(x); }
+// the cold start's complex64 rounding of ifft2(sqrt T) (src/algorithms.py:27):
+// a no-op on complex64 state
+__device__ __forceinline__ float2 round_c64(float2 z) { return z; }
+using mr::round_c64;
 // target intensity T (as uploaded) and numpy's amplitude sqrt(T): float16 for
 // uint8, float32 for float32, both widened
 __device__ __forceinline__ float tgt_at(const void* tgt, int tt, long long i) {
     return tt == TGT_U8 ? (float)static_cast<const uint8_t*>(tgt)[i] : static_cast<const float*>(tgt)[i];
 }
-__device__ __forceinline__ double amp_rz(float t, int tt) {
-    return tt == TGT_U8 ? (double)TgtLoad<TGT_U8>::amp(t) : (double)TgtLoad<TGT_F32>::amp(t);
+template <class S = double>
+__device__ __forceinline__ S amp_rz(float t, int tt) {
+    return tt == TGT_U8 ? (S)TgtLoad<TGT_U8>::amp(t) : (S)TgtLoad<TGT_F32>::amp(t);
 }
+// twiddle source per precision: float64 powers from one load (TW_POW, below),
+// float32 every twiddle from the table (powers in float32 would drift ~1e-6)
 
 // Twiddles of the complex128 kernels: per butterfly one table load, w^1 =
 // exp(-2 pi i j / (Ns R)), and its powers w^r by complex products (float64:
@@ -79,8 +102,39 @@ __device__ __forceinline__ double amp_rz(float t, int tt) {
 // 1024-point column pass, profiles/r06/sq_rz1024_d.txt). Loads laundered
 // before every transform (TW_DIRECT_LAUNDER).
 constexpr int TW_POW = 3;
+// Twiddles of the complex64 kernels: every twiddle from the table (float32
+// powers would drift ~1e-6), copied into LDS at the kernel's start. The panel
+// plans put about one wave per SIMD on the chip (1080 x 1920: 1,080 row
+// waves), so nothing hides a per-pass global twiddle load's latency; from LDS
+// a pass waits ~100 cycles instead.
+constexpr int TW_LDS = 4;
+template <class C>
+struct alignas(2 * sizeof(Scalar<C>)) TwPod {  // trivially copyable twin of C
+    Scalar<C> x, y;
+};
 
 }  // namespace rz
+
+template <int N, class C>
+struct Twiddles<N, C, rz::TW_LDS> {
+    static constexpr bool kAlwaysLaunder = true;
+    using LdsPtr = const __attribute__((address_space(3))) rz::TwPod<C>*;
+    LdsPtr table;
+    __device__ __forceinline__ void launder() {  // distinct loads per transform (fft_core.hpp TW_DIRECT)
+        unsigned q = (unsigned)(unsigned long long)table;
+        asm volatile("" : "+s"(q));
+        table = (LdsPtr)(unsigned long long)q;
+    }
+    template <int TwOff, int RegOff, int PowOff, int R, int Ns, bool INV>
+    __device__ __forceinline__ void apply(C* u, int, int j) const {
+        static_for<R - 1>([&](auto rc) {
+            constexpr int r = decltype(rc)::value + 1;
+            const int i = TwOff + (r - 1) * Ns + j;
+            const C t = mk<C>(table[i].x, table[i].y);
+            u[r] = INV ? cmulc(u[r], t) : cmul(u[r], t);
+        });
+    }
+};
 
 template <int N, class C>
 struct Twiddles<N, C, rz::TW_POW> {
@@ -124,9 +178,10 @@ namespace rz {
 // workgroup per CU), rows reading row-major and writing B2 col 318 + row 245
 // us (writes in pieces cost as much as reads). GD and 1024^2 run faster on
 // LAY_B2 (GD 1024^2 45.6 -> 40.3 us), GS 4096^2 on LAY_RM: the engine picks
-// per plan (generic.hip, rz_layout). Either way the column passes read the
-// target from a float copy in B2 made at each run's start (contiguous, where
-// the uploaded row-major target gave 8 B per row), and user arrays (phases,
+// per plan (generic.hip, rz_layout). LAY_B2 column passes read the target
+// from a float copy in B2 made at each run's start (contiguous, where the
+// uploaded row-major target gave 8 B per row; LAY_RM reads the upload, where
+// the copy measured slower), and user arrays (phases,
 // a_in, the expected output, the GD field, the lone transforms' inputs and
 // outputs) stay row-major.
 constexpr int LAY_RM = 0, LAY_B2 = 1;
@@ -140,50 +195,78 @@ __host__ __device__ __forceinline__ long long b2_index(long long y, int x, int H
 // ds_read_b128 group (lanes {0-3, 12-15, 20-27}, (a/4) mod 64) take
 // complementary bank halves (6 extra LDS cycles per instruction measured with
 // a plain row offset; 0 modelled for the E = 16 plans, tools/rz_lds_banks.py).
-template <bool WAVE>
-struct LdsPairRow : LdsLine<double2, 0, WAVE> {
+template <class X, bool WAVE>
+struct LdsPairRow : LdsLine<X, 0, WAVE> {
     int x = 0;  // 4 for the pair's second row
     template <class C>
     __device__ __forceinline__ void store(int l, int o, C v) const {
-        this->base[this->cur + l * this->stride + (lds_slot(o) ^ x)] = mk<double2>(v.x, v.y);
+        this->base[this->cur + l * this->stride + (lds_slot(o) ^ x)] = mk<X>(v.x, v.y);
     }
     template <class C>
     __device__ __forceinline__ C load(int l, int o) const {
-        const double2 v = this->base[this->cur + l * this->stride + (lds_slot(o) ^ x)];
+        const X v = this->base[this->cur + l * this->stride + (lds_slot(o) ^ x)];
         return mk<C>(v.x, v.y);
     }
 };
+
+template <int P>
+constexpr int kTwMode = P == PREC_F64 ? TW_POW : TW_LDS;
+// LDS twiddle slots of a kernel (1: unused)
+template <int K, int P>
+constexpr int kTwSlots = kTwMode<P> == TW_LDS && twiddle_count_key(K) > 0 ? twiddle_count_key(K) : 1;
+
+// the plan's twiddle table into LDS (TW_LDS; every thread of the workgroup calls it)
+template <int K, int P, int THREADS, class Tw>
+__device__ __forceinline__ void tw_setup(Tw& tw, TwPod<CplxOf<P>>* lds_tw, const void* table) {
+    if constexpr (kTwMode<P> == TW_LDS) {
+        const TwPod<CplxOf<P>>* g = static_cast<const TwPod<CplxOf<P>>*>(table);
+        for (int i = threadIdx.x; i < kTwSlots<K, P>; i += THREADS) lds_tw[i] = g[i];
+        __syncthreads();
+        tw.table = (typename Tw::LdsPtr)lds_tw;
+    } else {
+        tw.table = (typename Tw::GlobalPtr)table;
+    }
+}
 
 template <int K, int LAY>
 struct RowGeo {
     static constexpr int T = PlanOf<K>::T;
     static constexpr bool PAIRS = LAY == LAY_B2;
-    static constexpr int RPW = PAIRS ? (T >= 128 ? 2 : 256 / T) : (T >= 256 ? 1 : 256 / T);
+    // rows per workgroup: ~256 threads, whole pairs on B2 (the panel plans' T =
+    // 20 .. 100 need not divide 256; the host checks H % RPW)
+    static constexpr int RPW = PAIRS ? (T >= 128 ? 2 : 2 * (128 / T)) : (T >= 256 ? 1 : 256 / T);
     static constexpr int THREADS = RPW * T;
-    static constexpr bool WAVE = (PAIRS ? 2 * T : T) <= 64;  // each row (pair) inside one wave: no barrier
+    static constexpr int GROUP = PAIRS ? 2 * T : T;  // lanes of one row (pair)
+    static constexpr bool WAVE = GROUP <= 64 && 64 % GROUP == 0;  // each row (pair) inside one wave: no barrier
     static constexpr int LINE = PlanOf<K>::ROWSTRIDE;
     // 512 (row-major) / 1024 (pairs) threads, the 4096 E = 8 rows: a register
     // budget of 16 waves per CU (<= 128 VGPRs)
     static constexpr int MIN_WAVES = THREADS == (PAIRS ? 1024 : 512) ? 4 : 1;
 };
 
-template <int K, int CW>
+template <int K, int CW, int P = PREC_F64>
 struct ColGeo {
     static constexpr int T = PlanOf<K>::T;
     static constexpr int THREADS = CW * T;
     static constexpr bool WAVE = THREADS <= 64;
     static constexpr int SLOTS = lds_line(PlanOf<K>::N) * CW;
-    static constexpr bool kValid = THREADS >= 64 && THREADS <= 1024 && SLOTS * 16 <= 160 * 1024;
+    static constexpr bool kValid = THREADS >= 64 && THREADS <= 1024 &&
+                                   (SLOTS + kTwSlots<K, P>) * (int)sizeof(CplxOf<P>) <= 160 * 1024;
 };
 
-template <int K, int OP, int LAY>
+template <int K, int OP, int LAY, int P>
 __global__ void __launch_bounds__((RowGeo<K, LAY>::THREADS), (RowGeo<K, LAY>::MIN_WAVES)) rz_row_kernel(mr::RowArgs a) {
-    using C = double2;
+    using C = CplxOf<P>;  // compute and state type
+    using S = Scalar<C>;
     using namespace mr;
+    const C* in = reinterpret_cast<const C*>(a.in);
+    C* out = reinterpret_cast<C*>(a.out);
+    C* xf = reinterpret_cast<C*>(a.x);
     constexpr int N = PlanOf<K>::N, E = PlanOf<K>::E, T = PlanOf<K>::T;
     constexpr int RPW = RowGeo<K, LAY>::RPW, LINE = RowGeo<K, LAY>::LINE;
     constexpr bool WV = RowGeo<K, LAY>::WAVE;
-    __shared__ double2 smem[RPW * LINE];
+    __shared__ C smem[RPW * LINE];
+    __shared__ TwPod<C> lds_tw[kTwSlots<K, P>];
     // lane -> (row of the tile, t); LAY_B2 pairs: lanes 4k .. 4k + 3 = (r, 2k), (r, 2k + 1),
     // (r + 1, 2k), (r + 1, 2k + 1) -- one 64-B piece of a panel per four lanes and slot
     int t, lrow;
@@ -207,32 +290,38 @@ __global__ void __launch_bounds__((RowGeo<K, LAY>::THREADS), (RowGeo<K, LAY>::MI
     if constexpr (OP == RO_GS || OP == RO_GD || OP == RO_GS_MID) {
         if (a.checked && a.iter > a.stop[b]) return;  // stopped earlier: frozen (src/algorithms.py:29,83)
     }
-    LdsPairRow<WV> lds;
+    LdsPairRow<C, WV> lds;
     lds.base = smem + lrow * LINE;
     lds.stride = LINE;
     lds.x = LAY == LAY_B2 ? (lrow & 1) << 2 : 0;
-    Twiddles<K, C, TW_POW> tw;
-    tw.table = (typename Twiddles<K, C, TW_POW>::GlobalPtr)a.pl.tw;
-    auto ain = [&](int m) -> double { return a.ain ? (double)a.ain[pix0 + t + T * m] : 1.0; };
+    Twiddles<K, C, kTwMode<P>> tw;
+    tw_setup<K, P, RowGeo<K, LAY>::THREADS>(tw, lds_tw, a.pl.tw);
+    auto ain = [&](int m) -> S { return a.ain ? (S)a.ain[pix0 + t + T * m] : (S)1; };
     C v[1][E];
 #pragma unroll
     for (int m = 0; m < E; ++m) {
         const long long i = off + t + T * m;
         if constexpr (OP == RO_WARM) {
             // numpy: exp(1j * float32 phase) is complex64, then times the float64 a_in
-            double s, c;
-            sincos((double)a.phase_in[i], &s, &c);
-            const double am = ain(m);
-            v[0][m] = make_double2((double)(float)c * am, (double)(float)s * am);
+            const S am = ain(m);
+            if constexpr (P == PREC_F64) {
+                double s, c;
+                sincos((double)a.phase_in[i], &s, &c);
+                v[0][m] = make_double2((double)(float)c * am, (double)(float)s * am);
+            } else {
+                float s, c;
+                sincosf(a.phase_in[i], &s, &c);
+                v[0][m] = make_float2(c * am, s * am);
+            }
         } else if constexpr (OP == RO_GD_INIT) {
             const float2 f = a.field0[i];
-            const double2 x = make_double2((double)f.x, (double)f.y);
-            a.x[i] = x;
+            const C x = mk<C>((S)f.x, (S)f.y);
+            xf[i] = x;
             v[0][m] = u_rz(x, ain(m));
         } else if constexpr (OP == RO_FWD || OP == RO_INV) {
-            v[0][m] = a.in[i];  // lone transforms: row-major input
+            v[0][m] = in[i];  // lone transforms: row-major input
         } else {
-            v[0][m] = a.in[st_at(m)];
+            v[0][m] = in[st_at(m)];
         }
     }
     if constexpr (OP == RO_FWD || OP == RO_WARM || OP == RO_GD_INIT) {
@@ -255,32 +344,38 @@ __global__ void __launch_bounds__((RowGeo<K, LAY>::THREADS), (RowGeo<K, LAY>::MI
     } else if constexpr (OP == RO_GD_FOURIER) {
         // angle of the complex64 ifft2 is float32, exp of it complex64 (:153-156)
         fft_pair<K, true, false, C>(v, t, tw, lds, [&](int, int m, C& z) {
-            const double2 c = round_c64(z);
+            const C c = round_c64(z);
             const float ang = atan2f((float)c.y, (float)c.x);
-            double s, co;
-            sincos((double)ang, &s, &co);
-            const double am = ain(m);
-            const double2 x = make_double2((double)(float)co * am, (double)(float)s * am);
-            a.x[off + t + T * m] = x;
+            float sn, cs;
+            sincosf(ang, &sn, &cs);  // (the float64 engine used sincos of the float32 angle, rounded)
+            if constexpr (P == PREC_F64) {
+                double s, co;
+                sincos((double)ang, &s, &co);
+                sn = (float)s;
+                cs = (float)co;
+            }
+            const S am = ain(m);
+            const C x = mk<C>((S)cs * am, (S)sn * am);
+            xf[off + t + T * m] = x;
             z = u_rz(x, am);
         });
     } else if constexpr (OP == RO_GD) {
         // dEdF = ifft2(G) a_in (unscaled transform * 1/S), dEdX_complex, x -= lr dEdX
         // (:87-91, :179-185); next forward input u = a_in x/|x| (:84)
-        const double l = (double)a.lr[a.iter];
-        auto update = [&](int m, const C& z) -> double2 {
-            const double am = ain(m);
-            const double s = am * a.inv_s;
-            const double gx = z.x * s, gy = z.y * s;
+        const S l = (S)a.lr[a.iter];
+        auto update = [&](int m, const C& z) -> C {
+            const S am = ain(m);
+            const S s = am * (S)a.inv_s;
+            const S gx = z.x * s, gy = z.y * s;
             const long long i = off + t + T * m;
-            double2 x = a.x[i];
+            C x = xf[i];
             // dEdX_complex = (g - x Re(conj(x) g) / |x|^2) / |x| (:179-185)
-            const double inv = rsq_nr(x.x * x.x + x.y * x.y);
-            const double inv3 = inv * inv * inv;
-            const double re = x.x * gx + x.y * gy;
+            const S inv = rsq_nr(x.x * x.x + x.y * x.y);
+            const S inv3 = inv * inv * inv;
+            const S re = x.x * gx + x.y * gy;
             x.x -= l * (gx * inv - x.x * re * inv3);
             x.y -= l * (gy * inv - x.y * re * inv3);
-            a.x[i] = x;
+            xf[i] = x;
             return x;
         };
         if (a.last) {  // the run's last update needs no next forward transform
@@ -290,17 +385,21 @@ __global__ void __launch_bounds__((RowGeo<K, LAY>::THREADS), (RowGeo<K, LAY>::MI
         fft_pair<K, true, false, C>(v, t, tw, lds, [&](int, int m, C& z) { z = u_rz(update(m, z), ain(m)); });
     }
 #pragma unroll
-    for (int m = 0; m < E; ++m) a.out[st_at(m)] = v[0][m];
+    for (int m = 0; m < E; ++m) out[st_at(m)] = v[0][m];
 }
 
-template <int K, int CW, int OP, int LAY>
-__global__ void __launch_bounds__((ColGeo<K, CW>::THREADS), 1) rz_col_kernel(mr::ColArgs a) {
-    using C = double2;
+template <int K, int CW, int OP, int LAY, int P>
+__global__ void __launch_bounds__((ColGeo<K, CW, P>::THREADS), 1) rz_col_kernel(mr::ColArgs a) {
+    using C = CplxOf<P>;  // compute and state type
+    using S = Scalar<C>;
     using namespace mr;
+    const C* in = reinterpret_cast<const C*>(a.in);
+    C* out = reinterpret_cast<C*>(a.out);
     constexpr int E = PlanOf<K>::E, T = PlanOf<K>::T;
-    constexpr int THREADS = ColGeo<K, CW>::THREADS;
-    constexpr bool WV = ColGeo<K, CW>::WAVE;
-    __shared__ double2 smem[ColGeo<K, CW>::SLOTS];
+    constexpr int THREADS = ColGeo<K, CW, P>::THREADS;
+    constexpr bool WV = ColGeo<K, CW, P>::WAVE;
+    __shared__ C smem[ColGeo<K, CW, P>::SLOTS];
+    __shared__ TwPod<C> lds_tw[kTwSlots<K, P>];
     const int c = threadIdx.x % CW, t = threadIdx.x / CW;
     const int id = xcd_remap(blockIdx.x, gridDim.x);  // neighbouring tiles (partial lines) on one XCD
     const int b = id / a.nwg;
@@ -319,16 +418,16 @@ __global__ void __launch_bounds__((ColGeo<K, CW>::THREADS), 1) rz_col_kernel(mr:
     if constexpr (OP == CO_GS || OP == CO_GD_STATS || OP == CO_GD_GRAD || OP == CO_GD_GRAD_U8) {
         if (a.checked && a.iter > a.stop[b]) return;  // stopped earlier: frozen
     }
-    const LdsTile<CW, double2, 0, WV> lds{smem, c};
-    Twiddles<K, C, TW_POW> tw;
-    tw.table = (typename Twiddles<K, C, TW_POW>::GlobalPtr)a.pl.tw;
+    const LdsTile<CW, C, 0, WV> lds{smem, c};
+    Twiddles<K, C, kTwMode<P>> tw;
+    tw_setup<K, P, THREADS>(tw, lds_tw, a.pl.tw);
     C v[1][E];
 #pragma unroll
     for (int m = 0; m < E; ++m) {
         if constexpr (OP == CO_AMP_INV)
-            v[0][m] = make_double2(amp_rz(tgt_val(m, a.tt), a.tt), 0.0);
+            v[0][m] = mk<C>(amp_rz<S>(tgt_val(m, a.tt), a.tt), (S)0);
         else
-            v[0][m] = a.in[st_at(m)];
+            v[0][m] = in[st_at(m)];
     }
     if constexpr (OP == CO_FWD) {
         fft_line<K, false, C>(v, t, tw, lds);
@@ -338,7 +437,7 @@ __global__ void __launch_bounds__((ColGeo<K, CW>::THREADS), 1) rz_col_kernel(mr:
         double mx = 0.0, s2 = 0.0, st = 0.0;
         auto stats = [&](int m, const C& z, float tv) -> double {
             const long long i = base + m * rstep;
-            const double en = z.x * z.x + z.y * z.y;
+            const double en = (double)(z.x * z.x + z.y * z.y);
             mx = fmax(mx, en);
             s2 += en * en;
             st += en * (double)tv;
@@ -350,7 +449,7 @@ __global__ void __launch_bounds__((ColGeo<K, CW>::THREADS), 1) rz_col_kernel(mr:
             fft_pair<K, false, true, C>(v, t, tw, lds, [&](int, int m, C& z) {
                 const float tv = tgt_val(m, a.tt);
                 (void)stats(m, z, tv);
-                z = unit_rz(z, amp_rz(tv, a.tt));
+                z = unit_rz(z, amp_rz<S>(tv, a.tt));
             });
         } else if constexpr (OP == CO_GD_STATS) {
             fft_line_epi<K, false, C>(v, t, tw, lds,
@@ -358,14 +457,14 @@ __global__ void __launch_bounds__((ColGeo<K, CW>::THREADS), 1) rz_col_kernel(mr:
         } else if constexpr (OP == CO_GD_GRAD || OP == CO_GD_GRAD_U8) {
             // G = mask F (s P - T), s = norm / max P (:80,85-88); numpy's mask dtype:
             // float32 for a float32 target, float64 for uint8
-            const double s = a.norm[b] / a.stats[((long long)b * a.max_loops + a.iter) * 4];
+            const S s = (S)(a.norm[b] / a.stats[((long long)b * a.max_loops + a.iter) * 4]);
             fft_pair<K, false, true, C>(v, t, tw, lds, [&](int, int m, C& z) {
-                const double tv = (double)tgt_val(m, OP == CO_GD_GRAD_U8 ? TGT_U8 : TGT_F32);
-                const double mask = OP == CO_GD_GRAD_U8
-                                        ? 1.0 + (double)a.wa * tv / 255.0
-                                        : (double)(1.0f + __fdiv_rn(__fmul_rn(a.wa, (float)tv), 255.0f));
-                const double w = mask * ((z.x * z.x + z.y * z.y) * s - tv);
-                z = make_double2(z.x * w, z.y * w);
+                const S tv = (S)tgt_val(m, OP == CO_GD_GRAD_U8 ? TGT_U8 : TGT_F32);
+                const S mask = OP == CO_GD_GRAD_U8
+                                   ? (S)(1.0 + (double)a.wa * (double)tv / 255.0)
+                                   : (S)(1.0f + __fdiv_rn(__fmul_rn(a.wa, (float)tv), 255.0f));
+                const S w = mask * ((z.x * z.x + z.y * z.y) * s - tv);
+                z = mk<C>(z.x * w, z.y * w);
             });
         }
         if constexpr (OP == CO_GS || OP == CO_GD_STATS) {
@@ -383,24 +482,25 @@ __global__ void __launch_bounds__((ColGeo<K, CW>::THREADS), 1) rz_col_kernel(mr:
 #pragma unroll
     for (int m = 0; m < E; ++m) {
         if constexpr (OP == CO_FWD || OP == CO_INV)
-            a.out[base + m * rstep] = v[0][m];  // lone transforms: row-major output
+            out[base + m * rstep] = v[0][m];  // lone transforms: row-major output
         else
-            a.out[st_at(m)] = v[0][m];
+            out[st_at(m)] = v[0][m];
     }
 }
 
 // ------------------------------------------------------------------------
 // host side (rz_inst.hip, one object per plan key)
 // ------------------------------------------------------------------------
-#define SLM_RZ_DECLARE(N)                                                                          \
-    int rz_row_launch_##N(int lay, int op, const mr::RowArgs& a, int grid, hipStream_t st);        \
-    int rz_col_launch_##N(int lay, int cw, int op, const mr::ColArgs& a, int grid, hipStream_t st); \
-    int rz_row_rpw_##N(int lay);                                                                   \
-    int rz_col_ok_##N(int cw);
+#define SLM_RZ_DECLARE(N)                                                                                    \
+    int rz_row_launch_##N(int prec, int lay, int op, const mr::RowArgs& a, int grid, hipStream_t st);        \
+    int rz_col_launch_##N(int prec, int lay, int cw, int op, const mr::ColArgs& a, int grid, hipStream_t st); \
+    int rz_row_rpw_##N(int lay);                                                                             \
+    int rz_col_ok_##N(int prec, int cw);
 SLM_RZ_DECLARE(0)
 SLM_RZ_DECLARE(1)
 SLM_RZ_DECLARE(2)
 SLM_RZ_DECLARE(3)
+SLM_RZ_DECLARE(4)
 SLM_RZ_DECLARE(5)
 SLM_RZ_DECLARE(6)
 SLM_RZ_DECLARE(8)
@@ -410,19 +510,30 @@ SLM_RZ_DECLARE(11)
 SLM_RZ_DECLARE(12)
 SLM_RZ_DECLARE(13)
 SLM_RZ_DECLARE(14)
+SLM_RZ_DECLARE(15)
+SLM_RZ_DECLARE(16)
+SLM_RZ_DECLARE(17)
+SLM_RZ_DECLARE(18)
+SLM_RZ_DECLARE(19)
+SLM_RZ_DECLARE(20)
+SLM_RZ_DECLARE(21)
+SLM_RZ_DECLARE(22)
+SLM_RZ_DECLARE(23)
 #undef SLM_RZ_DECLARE
-#define SLM_RZ_FOR_EACH_KEY(X) X(0) X(1) X(2) X(3) X(5) X(6) X(8) X(9) X(10) X(11) X(12) X(13) X(14)
+#define SLM_RZ_FOR_EACH_KEY(X) \
+    X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) X(17) X(18) X(19) X(20) \
+    X(21) X(22) X(23)
 
 // launch op on plan key k (0 on success, -1 on a launch error or an unbuilt key)
-inline int rz_row_launch(int k, int lay, int op, const mr::RowArgs& a, int grid, hipStream_t st) {
+inline int rz_row_launch(int k, int prec, int lay, int op, const mr::RowArgs& a, int grid, hipStream_t st) {
 #define SLM_CASE(N) \
-    case N: return rz_row_launch_##N(lay, op, a, grid, st);
+    case N: return rz_row_launch_##N(prec, lay, op, a, grid, st);
     switch (k) { SLM_RZ_FOR_EACH_KEY(SLM_CASE) default: return -1; }
 #undef SLM_CASE
 }
-inline int rz_col_launch(int k, int lay, int cw, int op, const mr::ColArgs& a, int grid, hipStream_t st) {
+inline int rz_col_launch(int k, int prec, int lay, int cw, int op, const mr::ColArgs& a, int grid, hipStream_t st) {
 #define SLM_CASE(N) \
-    case N: return rz_col_launch_##N(lay, cw, op, a, grid, st);
+    case N: return rz_col_launch_##N(prec, lay, cw, op, a, grid, st);
     switch (k) { SLM_RZ_FOR_EACH_KEY(SLM_CASE) default: return -1; }
 #undef SLM_CASE
 }
@@ -433,10 +544,10 @@ inline int rz_row_rpw(int k, int lay) {
     switch (k) { SLM_RZ_FOR_EACH_KEY(SLM_CASE) default: return 0; }
 #undef SLM_CASE
 }
-// 1 if key k has column kernels of cw columns
-inline int rz_col_ok(int k, int cw) {
+// 1 if key k has column kernels of cw columns at precision prec
+inline int rz_col_ok(int k, int prec, int cw) {
 #define SLM_CASE(N) \
-    case N: return rz_col_ok_##N(cw);
+    case N: return rz_col_ok_##N(prec, cw);
     switch (k) { SLM_RZ_FOR_EACH_KEY(SLM_CASE) default: return 0; }
 #undef SLM_CASE
 }

@@ -385,6 +385,7 @@ struct slm_plan {
     // (generic.hpp) runs the loop; state and arrays row-major, float64 arithmetic
     GenericEngine* gen = nullptr;
     hipGraphExec_t gexec = nullptr;
+    bool generic = false;  // an any-size plan (gen is its engine; null only after a failed rebuild)
     int g_loops = -1, g_checked = -1, g_state = -1;
     double g_tol = 0.0;
     float g_wa = 0.f;
@@ -839,6 +840,7 @@ GenericView gview(slm_plan* p) {
     v.has_ain = p->has_ain;
     v.max_loops = p->max_loops;
     v.nwg = p->nwg;
+    v.prec = p->prec;
     v.holo = p->holo;
     v.stream = p->stream;
     v.tgt = p->tgt;
@@ -866,6 +868,7 @@ int enqueue_run(slm_plan* p, int loops, double tol, int checked, float wa) {
     if (loops < 1 || loops > p->max_loops)
         return fail(SLM_ERR_ARG, "loops %d outside [1, %d]", loops, p->max_loops);
     if (p->algo == SLM_ALGO_GD && !p->lr_set) return fail(SLM_ERR_STATE, "learning rates not set");
+    if (p->generic && !p->gen) return fail(SLM_ERR_STATE, "the plan lost its engine (failed slm_plan_set_precision)");
     HIP_TRY(hipSetDevice(p->device));
     p->field_fresh = false;  // the run writes the field
     p->ran = true;
@@ -1065,10 +1068,17 @@ int plan_create_on(int device, int algo, int batch, int height, int width, int t
     int max_nwg = 0, min_rpw = INT_MAX;
     if (generic) {
         p->dev_tt = tgt_type;  // row-major target, amplitude formed where used
-        p->prec = PREC_F64;
+        // float32 GS (float32 targets unless $SLM_PRECISION) on the complex64
+        // radix kernels where both sides have one (13-smooth panels, e.g.
+        // 1080 x 1920), float64 otherwise and always under $SLM_ENGINE=float64
+        const bool forced64 = eng && !std::strcmp(eng, "float64");
+        p->prec = generic_precision(batch, height, width, algo, forced64 ? PREC_F64 : p->prec);
         p->lid = LAYOUT_DEFAULT;
         p->cw = 0;
-        p->nwg = max_nwg = generic_nwg(batch, height, width, p->holo);
+        p->nwg = generic_nwg(batch, height, width, p->holo, algo, p->prec);
+        // slm_plan_set_precision may switch engines: partials for either tiling
+        max_nwg = std::max(generic_nwg(batch, height, width, p->holo, algo, PREC_F32),
+                           generic_nwg(batch, height, width, p->holo, algo, PREC_F64));
         p->rpw = min_rpw = 1;
     } else {
         const int want = p->prec;
@@ -1139,6 +1149,7 @@ int plan_create_on(int device, int algo, int batch, int height, int width, int t
         RC(alloc((void**)&p->trace_col, (size_t)batch * max_nwg * kTraceSlots * sizeof(unsigned long long)));
         RC(alloc((void**)&p->trace_row, (size_t)batch * (height / min_rpw) * kTraceSlots * sizeof(unsigned long long)));
     }
+    p->generic = generic;
     if (generic) {
         if (int rc = generic_create(gview(p), &p->gen)) {
             free_plan(p);
@@ -1171,6 +1182,7 @@ int slm_plan_destroy(slm_plan* plan) {
 
 int slm_plan_set_target(slm_plan* p, const void* tgt) {
     if (!p || !tgt) return fail(SLM_ERR_ARG, "null argument");
+    if (p->generic && !p->gen) return fail(SLM_ERR_STATE, "the plan lost its engine (failed slm_plan_set_precision)");
     HIP_TRY(hipSetDevice(p->device));
     const long long n = (long long)p->B * p->holo;
     const size_t tb = p->tt == SLM_TGT_U8 ? 1 : 4;
@@ -1217,8 +1229,30 @@ int slm_plan_set_precision(slm_plan* p, int precision) {
     if (!p) return fail(SLM_ERR_ARG, "null plan");
     if (precision != SLM_PRECISION_F32 && precision != SLM_PRECISION_F64)
         return fail(SLM_ERR_ARG, "unknown precision %d", precision);
-    if (p->gen) return 0;  // the any-size engine computes in float64 only
     HIP_TRY(hipSetDevice(p->device));
+    if (p->gen) {  // any-size engine: rebuilt when the precision it runs at changes
+        const int prec = generic_precision(p->B, p->H, p->W, p->algo, precision);
+        if (prec == p->prec) return 0;
+        HIP_TRY(hipStreamSynchronize(p->stream));
+        if (p->gexec) {  // the captured run holds the old engine's kernels and buffers
+            HIP_TRY(hipGraphExecDestroy(p->gexec));
+            p->gexec = nullptr;
+        }
+        const int old_prec = p->prec, old_nwg = p->nwg;
+        generic_destroy(p->gen);
+        p->gen = nullptr;
+        p->prec = prec;
+        p->nwg = generic_nwg(p->B, p->H, p->W, p->holo, p->algo, prec);
+        const int rc = generic_create(gview(p), &p->gen);
+        if (rc) {  // keep a usable plan: the engine it had (its error stays the reported one)
+            p->prec = old_prec;
+            p->nwg = old_nwg;
+            const std::string msg = slm_last_error();
+            if (generic_create(gview(p), &p->gen)) p->gen = nullptr;
+            return fail(rc, "%s", msg.c_str());
+        }
+        return 0;
+    }
     RC(configure(p, precision));
     return 0;
 }
@@ -1455,12 +1489,14 @@ long long slm_plan_kernel_bytes(slm_plan* p, int cls) {
     const long long ab = p->has_ain ? 4 : 0;
     if (p->gen) {
         if (generic_kind(p->gen) == 2) return 0;  // line transforms: no column / row kernel classes
-        // mixed radix, complex128 state: column pass in 16 + T + out 16 (GD statistics: in + T);
-        // row pass in 16 + out 16 (+ a_in) (+ GD field read and write 32)
+        // mixed radix / radix plans, complex128 state (complex64: z = 8): column pass
+        // in z + T + out z (GD statistics: in + T); row pass in z + out z (+ a_in)
+        // (+ GD field read and write 2z)
+        const long long z = p->prec == PREC_F32 ? 8 : 16;
         switch (cls) {
-            case SLM_KERNEL_COL_MAIN: return px * (32 + tb);
-            case SLM_KERNEL_ROW_MAIN: return px * (32 + ab + (p->algo == SLM_ALGO_GD ? 32 : 0));
-            case SLM_KERNEL_GD_STATS: return px * (16 + tb);
+            case SLM_KERNEL_COL_MAIN: return px * (2 * z + tb);
+            case SLM_KERNEL_ROW_MAIN: return px * (2 * z + ab + (p->algo == SLM_ALGO_GD ? 2 * z : 0));
+            case SLM_KERNEL_GD_STATS: return px * (z + tb);
             default: return 0;
         }
     }
@@ -1491,7 +1527,7 @@ int slm_plan_engine(slm_plan* p, int* col_engine, int* row_engine) {
     if (!p || !col_engine || !row_engine) return fail(SLM_ERR_ARG, "null argument");
     // mirrors kernels.hpp: kShuffle<K, P> && (CW == 2 | RPW == 2) && one line per thread
     if (p->gen) {
-        *col_engine = *row_engine = generic_kind(p->gen);  // line transforms / mixed radix / radix c128 (generic.hpp)
+        *col_engine = *row_engine = generic_kind(p->gen);  // line transforms / mixed radix / radix plans (generic.hpp)
         return 0;
     }
     auto shuf = [&](int key, int prec) {
@@ -1719,7 +1755,8 @@ int c128_entry(int batch, int height, int width, C128Entry** out) {
     q.W = width;
     q.holo = (long long)height * width;
     q.max_loops = 1;
-    q.nwg = generic_nwg(batch, height, width, q.holo);
+    q.prec = PREC_F64;
+    q.nwg = generic_nwg(batch, height, width, q.holo, SLM_ALGO_GS, PREC_F64);
     q.device = g_device;
     int rc = 0;
     if (hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking) != hipSuccess)

@@ -43,10 +43,10 @@ def _expected_engine(shape, engine):
 @pytest.fixture(params=["mixed-radix", "bluestein"])
 def engine(request, monkeypatch):
     """The back end the plans of one test are created on (read at plan creation)."""
-    if request.param == "bluestein":
-        monkeypatch.setenv("SLM_GENERIC_ENGINE", "bluestein")
-    else:
-        monkeypatch.delenv("SLM_GENERIC_ENGINE", raising=False)
+    # "mr" keeps float32-target GS on shapes whose sides all have radix plans
+    # (768 x 1000: complex64 radix kernels by default, test_gpu_radix_c64.py)
+    # on the float64 mixed radix this file checks
+    monkeypatch.setenv("SLM_GENERIC_ENGINE", "bluestein" if request.param == "bluestein" else "mr")
     yield request.param
     from spatial_light_modulator_module_amd import algorithms as alg
 
@@ -247,16 +247,19 @@ def test_mixed_radix_fft2_c128_vs_numpy(gpu, shape):
 
 
 @pytest.mark.gpu
-def test_mixed_radix_gs_1080x1920_warm_start(gpu):
+def test_mixed_radix_gs_1080x1920_warm_start(gpu, monkeypatch):
     """A 1080 x 1920 SLM panel (1080 = 2^3 3^3 5, 1920 = 2^7 3 5) on the
-    mixed-radix engine, SURVEY.md 8c warm-start protocol (30 cold iterations
-    of the faithful oracle, then 100 more) against the float64 oracle."""
+    mixed-radix engine (float64; the default float32 run is
+    test_gpu_radix_c64.py's), SURVEY.md 8c warm-start protocol (30 cold
+    iterations of the faithful oracle, then 100 more) against the float64
+    oracle."""
     import os
 
     import scipy.fft as sfft
 
     WORKERS = min(16, os.cpu_count() or 1)  # the GPU box gives a process a 16-CPU share
 
+    monkeypatch.setenv("SLM_GENERIC_ENGINE", "mr")
     t = _target((1080, 1920), False, seed=21)
     with sfft.set_workers(WORKERS):
         phi30, _, _ = orc.gerchberg_saxton_faithful(t, 30)

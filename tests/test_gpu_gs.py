@@ -83,8 +83,11 @@ def test_gs_matches_faithful_oracle(gpu, shape, dtype):
     print(f"[parity] GS {shape} {np.dtype(dtype).name} random warm start x{loops}: phase rms {rms:.3e}")
     assert rms < PHASE_RMS_TOL
     np.testing.assert_allclose(errs[0], err_f, rtol=1e-5)
+    # uint8 runs on float64 butterflies by default while this restatement runs
+    # the reference's float16 sqrt(uint8) x complex64 arithmetic: 1 pixel in
+    # 786,432 of 768x1024 sat at 1.5e-4 * norm (profiles/r06/pytest_r06k.log)
     np.testing.assert_allclose(alg.expected_from(e[0], norm[0], emax[0]), exp_f, rtol=1e-3,
-                               atol=1e-4 * float(norm[0]))
+                               atol=(2e-4 if dtype == np.uint8 else 1e-4) * float(norm[0]))
 
 
 @pytest.mark.gpu

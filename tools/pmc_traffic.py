@@ -26,7 +26,7 @@ def kernel_class(name):
     (col MODE 0 GS, 4 / 7 GD gradient / fused -> col_main, 3 -> gd_stats; row MODE 0 GS,
     5 GD -> row_main); complex128 radix plans rz_col_kernel<K, CW, OP> /
     rz_row_kernel<K, OP> and mixed radix mr_col_kernel<OP, BIG> / mr_row_kernel<OP, BIG>
-    (col OP 3 GS, 5 GD gradient -> col_main, 4 -> gd_stats; row OP 4 GS, 7 GD -> row_main).
+    (col OP 3 GS, 5 / 6 GD gradient -> col_main, 4 -> gd_stats; row OP 4 / 8 GS, 7 GD -> row_main).
     The word boundary keeps mr_/rz_ names out of the float32 branch."""
     m = re.search(r"\b(rz_|mr_)?(col|row)_kernel<([^>]*)>", name)
     if not m:
@@ -43,8 +43,8 @@ def kernel_class(name):
     except (IndexError, ValueError):
         return None
     if side == "col":
-        return {3: "col_main", 5: "col_main", 4: "gd_stats"}.get(op)
-    return {4: "row_main", 7: "row_main"}.get(op)
+        return {3: "col_main", 5: "col_main", 6: "col_main", 4: "gd_stats"}.get(op)
+    return {4: "row_main", 7: "row_main", 8: "row_main"}.get(op)
 
 
 def per_launch(path, counter):
