@@ -659,7 +659,16 @@ int mr_roots(hipStream_t st) {
 // wide|narrow|e8 force a variant (per axis for the last two).
 int rz_key(int n, long long elems, bool col, int prec) {
     const int wide = plan_index(n, 0), narrow = plan_index(n, 1), e8 = plan_index(n, 2), panel = plan_index(n, 3);
-    if (rz::key_built(panel, prec)) return panel;
+    if (rz::key_built(panel, prec)) {
+        // variant 4 (1920 = 8.16.15 on 240 threads) for rows, where it measured
+        // faster (1080 x 1920 row pass 30.1 -> 25.3 us), variant 3 for columns
+        // (1920 x 1080 column pass 36.0 against 39.8, profiles/r06/speed_c64_alt_q.txt);
+        // $SLM_RZ_PANEL=alt|main forces one
+        const int alt = plan_index(n, 4);
+        const char* a = std::getenv("SLM_RZ_PANEL");
+        const bool use_alt = a ? !std::strcmp(a, "alt") : !col;
+        return use_alt && rz::key_built(alt, prec) ? alt : panel;
+    }
     const bool w_ok = rz::key_built(wide, prec), n_ok = rz::key_built(narrow, prec), e_ok = rz::key_built(e8, prec);
     const char* s = std::getenv(col ? "SLM_RZ_COL_PLAN" : "SLM_RZ_ROW_PLAN");
     if (!s) s = std::getenv("SLM_RZ_PLAN");
@@ -682,7 +691,9 @@ int rz_key(int n, long long elems, bool col, int prec) {
 // 8-thread lines; $SLM_RZ_CW overrides.
 int rz_cw_of(int ckey, int W, int prec) {
     const int T = kPlans[ckey].n / kPlans[ckey].e;
-    int cw = T >= 128 ? 2 : T >= 16 ? 4 : 8;
+    // complex64 lines of 64+ threads: 2 (1080 x 1920 column pass 35.4 -> 25.4 us,
+    // 768 x 1280 18.7 -> 16.7 us with 4 -> 2 columns, profiles/r06/speed_c64_cw2_p.txt)
+    int cw = T >= (prec == PREC_F32 ? 64 : 128) ? 2 : T >= 16 ? 4 : 8;
     if (const char* e = std::getenv("SLM_RZ_CW")) cw = std::atoi(e);
     if (cw < 1 || W % cw || !rz::rz_col_ok(ckey, prec, cw)) return 0;
     return cw;
@@ -723,25 +734,29 @@ bool rz_shape(int B, int H, int W, RzChoice* c, int algo, int prec) {
 
 // Stockham twiddle table of a plan key (the float32 engine's layout,
 // slm_capi.hip get_twiddles: every pass after the first holds (R - 1) Ns
-// entries exp(-2 pi i j r / (Ns R)); float2 for the complex64 kernels) and the
-// identity order (natural in and out)
+// entries exp(-2 pi i j r / (Ns R)); a mixed plan appends the same for its
+// reversed pass order; float2 for the complex64 kernels) and the identity
+// order (natural in and out)
 int rz_plan_line(GenericEngine* g, int key, mr::LinePlan* pl, hipStream_t st) {
     const RadixPlan& rp = kPlans[key];
     std::vector<double> tw;
-    int ns = 1;
-    for (int k = 0; k < rp.npass; ++k) {
-        const int r_ = rp.r[k];
-        if (ns > 1) {
-            const long long L = (long long)ns * r_;
-            for (int r = 1; r < r_; ++r)
-                for (int j = 0; j < ns; ++j) {
-                    const long long q = ((long long)j * r) % L;
-                    const double ang = -2.0 * M_PI * (double)q / (double)L;
-                    tw.push_back(std::cos(ang));
-                    tw.push_back(std::sin(ang));
-                }
+    // the forward pass order, then (mixed plans) the reversed one the inverse runs
+    for (int rev = 0; rev < (plan_mixed(key) ? 2 : 1); ++rev) {
+        int ns = 1;
+        for (int k = 0; k < rp.npass; ++k) {
+            const int r_ = pass_radix(key, rev != 0, k);
+            if (ns > 1) {
+                const long long L = (long long)ns * r_;
+                for (int r = 1; r < r_; ++r)
+                    for (int j = 0; j < ns; ++j) {
+                        const long long q = ((long long)j * r) % L;
+                        const double ang = -2.0 * M_PI * (double)q / (double)L;
+                        tw.push_back(std::cos(ang));
+                        tw.push_back(std::sin(ang));
+                    }
+            }
+            ns *= r_;
         }
-        ns *= r_;
     }
     if (tw.empty()) {
         tw.push_back(1.0);

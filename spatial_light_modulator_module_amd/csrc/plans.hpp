@@ -17,6 +17,11 @@ struct RadixPlan {
     int variant;  // 0 = wide (16-24 elements per thread), 1 = narrow (twice the threads)
     int npass;    // number of Stockham passes
     int r[8];     // radices, first pass first
+    // Mixed plans (ep[0] != 0, complex64 radix kernels only, radix_c128.hpp):
+    // elements per thread of each pass; pass k runs n / ep[k] threads (the line
+    // has n / e of them, e = the smallest ep[k]), each holding whole radix-r[k]
+    // butterflies, and the inverse runs the passes in reverse order.
+    int ep[8];
 };
 
 // Lengths the library supports along either image axis. 768 = 3 * 256 is the
@@ -50,19 +55,26 @@ constexpr RadixPlan kPlans[] = {
     // per CU where the E = 16 plan holds 8
     {4096, 8, 2, 4, {8, 8, 8, 8}},
     // complex64 radix kernels of the any-size engine only (radix_c128.hpp at
-    // float32, variant 3): 13-smooth SLM panel sides. Every radix divides E
-    // (the Stockham slot model), so a side with the factors 3 and 5 needs a
-    // multiple of 15 elements per thread; first and last radix equal where the
-    // factors allow (fused projection, fft_pair).
-    {600, 30, 3, 3, {10, 6, 10}},
-    {800, 20, 3, 3, {20, 2, 20}},
+    // float32, variant 3): 13-smooth SLM panel sides, as mixed plans (ep[]:
+    // with one E for every pass, a side with the factors 3 and 5 needed a
+    // multiple of 15 elements per thread -- 1920 ran 2.2.2.30.2.2.2 on 64
+    // threads, 1080 6.5.6.6 on 36; profiles/r06/speed_c64_n.txt).
+    {600, 6, 3, 3, {10, 6, 10}, {10, 6, 10}},  // 100 threads (60 in the radix-10 passes)
+    {800, 8, 3, 3, {10, 8, 10}, {10, 8, 10}},  // 100 threads (80)
     {1000, 10, 3, 3, {10, 10, 10}},
-    {1080, 30, 3, 4, {6, 5, 6, 6}},
-    {1152, 24, 3, 3, {12, 8, 12}},
-    {1200, 30, 3, 4, {10, 2, 6, 10}},
-    {1280, 20, 3, 4, {4, 20, 4, 4}},
-    {1536, 24, 3, 3, {8, 24, 8}},
-    {1920, 30, 3, 7, {2, 2, 2, 30, 2, 2, 2}},
+    // 1080 = 12.6.15: 90 threads per line (72 in the radix-15 pass), 3 passes
+    // where the single-E plan 6.5.6.6 needed 30 elements on 36 threads
+    {1080, 12, 3, 3, {12, 6, 15}, {12, 12, 15}},
+    {1152, 8, 3, 3, {12, 8, 12}, {12, 8, 12}},  // 144 threads (96)
+    {1200, 10, 3, 3, {10, 12, 10}, {10, 12, 10}},  // 120 threads (100 in the radix-12 pass)
+    {1280, 10, 3, 3, {16, 5, 16}, {16, 10, 16}},  // 128 threads (80 in the radix-16 passes)
+    {1536, 12, 3, 3, {16, 6, 16}, {16, 12, 16}},  // 128 threads (96)
+    // 1920 = 15.16.8: 128 threads per line (120 in the radix-16 / 8 passes), 3
+    // passes where the single-E plan 2.2.2.30.2.2.2 ran 7 on 64 threads
+    {1920, 15, 3, 3, {15, 16, 8}, {15, 16, 16}},
+    // variant 4 (A/B, $SLM_RZ_PANEL=alt): 1920 = 8.16.15 on 240 threads (120 / 128
+    // in the radix-16 / 15 passes)
+    {1920, 8, 4, 3, {8, 16, 15}, {8, 16, 15}},
 };
 constexpr int kNumPlans = sizeof(kPlans) / sizeof(kPlans[0]);
 // plan keys of the float32 engine (kernels_inst.hip, dispatch.hpp, Makefile LENGTHS)
@@ -83,6 +95,24 @@ constexpr int twiddle_count_key(int key) {
         ns *= kPlans[key].r[k];
     }
     return total;
+}
+constexpr bool plan_mixed(int key) { return kPlans[key].ep[0] != 0; }
+// radix of pass p in transform order (mixed plans: the inverse runs backwards)
+constexpr int pass_radix(int key, bool rev, int p) {
+    return kPlans[key].r[rev ? kPlans[key].npass - 1 - p : p];
+}
+// the same table layout for the reversed pass order of a mixed plan, stored
+// after the forward order's entries
+constexpr int twiddle_count_rev(int key) {
+    int ns = 1, total = 0;
+    for (int k = 0; k < kPlans[key].npass; ++k) {
+        if (ns > 1) total += (pass_radix(key, true, k) - 1) * ns;
+        ns *= pass_radix(key, true, k);
+    }
+    return total;
+}
+constexpr int twiddle_count_all(int key) {
+    return twiddle_count_key(key) + (plan_mixed(key) ? twiddle_count_rev(key) : 0);
 }
 
 // Padded LDS footprint of one line (one extra complex slot per 16).

@@ -48,7 +48,7 @@ namespace rz {
 // multiple of 15 elements per thread).
 __host__ __device__ constexpr bool key_built(int k, int p = PREC_F64) {
     return k >= 0 && k < kNumPlans &&
-           (p == PREC_F64 ? kPlans[k].e <= 16 && kPlans[k].variant != 3 : kPlans[k].e <= 30);
+           (p == PREC_F64 ? kPlans[k].e <= 16 && kPlans[k].variant < 3 : kPlans[k].e <= 30);
 }
 
 // Element-wise float64 pieces of these kernels: the reference's exp(i angle z)
@@ -103,10 +103,9 @@ __device__ __forceinline__ S amp_rz(float t, int tt) {
 // before every transform (TW_DIRECT_LAUNDER).
 constexpr int TW_POW = 3;
 // Twiddles of the complex64 kernels: every twiddle from the table (float32
-// powers would drift ~1e-6), copied into LDS at the kernel's start. The panel
-// plans put about one wave per SIMD on the chip (1080 x 1920: 1,080 row
-// waves), so nothing hides a per-pass global twiddle load's latency; from LDS
-// a pass waits ~100 cycles instead.
+// powers would drift ~1e-6). TW_LDS copies the table into LDS at the kernel's
+// start (it served the single-E panel plans, one wave per SIMD; kept
+// selectable, kTwMode below).
 constexpr int TW_LDS = 4;
 template <class C>
 struct alignas(2 * sizeof(Scalar<C>)) TwPod {  // trivially copyable twin of C
@@ -209,11 +208,206 @@ struct LdsPairRow : LdsLine<X, 0, WAVE> {
     }
 };
 
+// complex64: table twiddles where used (TW_DIRECT_LAUNDER, L1/L2-resident);
+// the LDS copy (TW_LDS) measured slower once the mixed plans put 2-4 waves per
+// SIMD on the chip (1920 x 1080 42.5 against 54.4 us per GS iteration: the
+// copy of both pass orders doubled a 1920-point column tile's LDS;
+// profiles/r06/speed_c64_twg_r.txt)
 template <int P>
-constexpr int kTwMode = P == PREC_F64 ? TW_POW : TW_LDS;
-// LDS twiddle slots of a kernel (1: unused)
+constexpr int kTwMode = P == PREC_F64 ? TW_POW : TW_DIRECT_LAUNDER;
+// LDS twiddle slots of a kernel (1: unused; mixed plans hold both pass orders)
 template <int K, int P>
-constexpr int kTwSlots = kTwMode<P> == TW_LDS && twiddle_count_key(K) > 0 ? twiddle_count_key(K) : 1;
+constexpr int kTwSlots = kTwMode<P> == TW_LDS && twiddle_count_all(K) > 0 ? twiddle_count_all(K) : 1;
+
+// ------------------------------------------------------------------------
+// Mixed plans (plans.hpp ep[]): the elements per thread change from pass to
+// pass. A single-E Stockham plan needs every radix to divide E, so a
+// 1920-point line (2^7 3 5) with E = 30 has one factor 2 per pass: seven
+// passes on 64 threads, one wave per SIMD over a 1080 x 1920 panel
+// (profiles/r06/sq_c64_1080x1920_n.txt: 8,373 VALU and 906 LDS instructions
+// per wave). Here pass p holds E_p elements on T_p = N / E_p threads, slot m
+// of thread t being element t + T_p m as in the single-E driver; threads
+// t >= T_p sit the pass out. The forward transform runs the radices in plan
+// order, the inverse backwards, so the pair inverse -> forward (row kernels)
+// and forward -> inverse (column kernels) always meets on one radix and one
+// slot layout (fft_pair's fused projection).
+// ------------------------------------------------------------------------
+template <int K>
+constexpr int kTMax = PlanOf<K>::T;  // threads of a line (the smallest E_p)
+
+template <int K, bool INV, int P>
+struct MxPass {
+    static constexpr int NP = kPlans[K].npass;
+    static constexpr bool REV = INV && plan_mixed(K);
+    static constexpr int I = REV ? NP - 1 - P : P;
+    static constexpr int R = kPlans[K].r[I];
+    static constexpr int E = plan_mixed(K) ? kPlans[K].ep[I] : kPlans[K].e;
+    static constexpr int T = kPlans[K].n / E;
+    static constexpr bool LAST = P == NP - 1;
+    static constexpr int ns_at() {
+        int ns = 1;
+        for (int q = 0; q < P; ++q) ns *= pass_radix(K, REV, q);
+        return ns;
+    }
+    static constexpr int tw_at() {  // table offset of this pass's entries
+        int ns = 1, off = REV ? twiddle_count_key(K) : 0;
+        for (int q = 0; q < P; ++q) {
+            if (ns > 1) off += (pass_radix(K, REV, q) - 1) * ns;
+            ns *= pass_radix(K, REV, q);
+        }
+        return off;
+    }
+    static constexpr int NS = ns_at();
+    static constexpr int TWOFF = tw_at();
+    static_assert(E % R == 0 && T * E == kPlans[K].n, "mixed plan: radix must divide the pass's elements");
+    static_assert(T <= kTMax<K>, "mixed plan: e must be the smallest ep");
+};
+// slot layout at a transform's ends: elements per thread and threads per line
+template <int K, bool INV, bool FIRST>
+using MxEnd = MxPass<K, INV, FIRST ? 0 : kPlans[K].npass - 1>;
+// register slots a kernel's line array needs
+template <int K>
+constexpr int mx_emax() {
+    int e = kPlans[K].e;
+    if (plan_mixed(K))
+        for (int q = 0; q < kPlans[K].npass; ++q) e = kPlans[K].ep[q] > e ? kPlans[K].ep[q] : e;
+    return e;
+}
+template <int K>
+constexpr int kEMax = mx_emax<K>();
+
+template <int K, bool INV, int P, class C, class V, int EM, class Lds, class Tw, class Sink>
+__device__ __forceinline__ void mx_from(V (&v)[1][EM], int t, const Tw& tw, const Lds& lds, Sink& sink) {
+    using Ps = MxPass<K, INV, P>;
+    constexpr int R = Ps::R, E = Ps::E, T = Ps::T, Ns = Ps::NS, NB = E / R;
+    asm volatile("" : "+v"(t));  // per-pass address arithmetic (stockham_from)
+    if (T == kTMax<K> || t < T) {
+        static_for<NB>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            const int b = t + k * T;
+            const int j = (Ns == 1) ? 0 : (b % Ns);
+            C u[R];
+            static_for<R>([&](auto rc) {
+                constexpr int r = decltype(rc)::value;
+                u[r] = cv<C>(v[0][k + r * NB]);
+            });
+            if constexpr (Ns > 1) tw.template apply<Ps::TWOFF, 0, 0, R, Ns, INV>(u, k, j);
+            Dft<R, INV, C>::run(u);
+            if constexpr (Ps::LAST) {
+                sink(kc, u);
+            } else {
+                const int o = (b / Ns) * Ns * R + j;
+                static_for<R>([&](auto rc) {
+                    constexpr int r = decltype(rc)::value;
+                    lds.store(0, o + r * Ns, u[r]);
+                });
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        });
+    }
+    if constexpr (!Ps::LAST) {
+        using Pn = MxPass<K, INV, P + 1>;
+        exchange_sync(lds);
+        if (Pn::T == kTMax<K> || t < Pn::T) {
+            static_for<Pn::E>([&](auto mc) {
+                constexpr int m = decltype(mc)::value;
+                v[0][m] = lds.template load<V>(0, t + m * Pn::T);
+            });
+        }
+        exchange_done(lds);
+        mx_from<K, INV, P + 1, C>(v, t, tw, lds, sink);
+    }
+}
+
+// Transform wrappers of the radix kernels: epi(p, z) sees each output z with
+// its element position p along the line (single-E plans: fft_core.hpp's
+// drivers, slot m of thread t at p = t + T m; mixed plans: mx_from).
+template <int K, bool INV, class C, class V, int EM, class Lds, class Tw>
+__device__ __forceinline__ void rz_line(V (&v)[1][EM], int t, const Tw& tw0, const Lds& lds) {
+    if constexpr (plan_mixed(K)) {
+        Tw tw = tw0;
+        tw.launder();
+        using PL = MxEnd<K, INV, false>;
+        auto wb = [&](auto kc, auto& u) {
+            constexpr int k = decltype(kc)::value, NB = PL::E / PL::R;
+            static_for<PL::R>([&](auto rc) {
+                constexpr int r = decltype(rc)::value;
+                v[0][k + r * NB] = cv<V>(u[r]);
+            });
+        };
+        mx_from<K, INV, 0, C>(v, t, tw, lds, wb);
+    } else {
+        fft_line<K, INV, C>(v, t, tw0, lds);
+    }
+}
+template <int K, bool INV, class C, class V, int EM, class Lds, class Tw, class Epi>
+__device__ __forceinline__ void rz_line_epi(V (&v)[1][EM], int t, const Tw& tw0, const Lds& lds, Epi&& epi) {
+    if constexpr (plan_mixed(K)) {
+        Tw tw = tw0;
+        tw.launder();
+        using PL = MxEnd<K, INV, false>;
+        auto sink = [&](auto kc, auto& u) {
+            constexpr int k = decltype(kc)::value, NB = PL::E / PL::R;
+            static_for<PL::R>([&](auto rc) {
+                constexpr int r = decltype(rc)::value;
+                epi(t + PL::T * (k + r * NB), u[r]);
+                v[0][k + r * NB] = cv<V>(u[r]);
+            });
+        };
+        mx_from<K, INV, 0, C>(v, t, tw, lds, sink);
+    } else {
+        constexpr int T = PlanOf<K>::T;
+        fft_line_epi<K, INV, C>(v, t, tw0, lds, [&](int, int m, C& z) { epi(t + T * m, z); });
+    }
+}
+template <int K, bool INV1, bool INV2, class C, class V, int EM, class Lds, class Tw, class Epi>
+__device__ __forceinline__ void rz_pair(V (&v)[1][EM], int t, const Tw& tw0, const Lds& lds, Epi&& epi) {
+    if constexpr (plan_mixed(K)) {
+        static_assert(INV1 != INV2, "a mixed pair runs one transform forwards and the other backwards");
+        using PL = MxEnd<K, INV1, false>;  // the first transform's last pass ...
+        using PF = MxEnd<K, INV2, true>;   // ... is the second one's first (same radix and slots)
+        static_assert(PL::R == PF::R && PL::E == PF::E, "mixed pair: passes do not meet");
+        Tw tw = tw0;
+        tw.launder();
+        auto sink = [&](auto kc, auto& u) {
+            constexpr int k = decltype(kc)::value, NB = PL::E / PL::R;
+            static_for<PL::R>([&](auto rc) {
+                constexpr int r = decltype(rc)::value;
+                epi(t + PL::T * (k + r * NB), u[r]);
+            });
+            Dft<PL::R, INV2, C>::run(u);  // the second transform's first pass: Ns = 1, no twiddles
+            const int o = (t + k * PL::T) * PL::R;
+            static_for<PL::R>([&](auto rc) {
+                constexpr int r = decltype(rc)::value;
+                lds.store(0, o + r, u[r]);
+            });
+        };
+        mx_from<K, INV1, 0, C>(v, t, tw, lds, sink);
+        using P1 = MxPass<K, INV2, 1>;
+        exchange_sync(lds);
+        if (P1::T == kTMax<K> || t < P1::T) {
+            static_for<P1::E>([&](auto mc) {
+                constexpr int m = decltype(mc)::value;
+                v[0][m] = lds.template load<V>(0, t + m * P1::T);
+            });
+        }
+        exchange_done(lds);
+        Tw tw2 = tw0;
+        tw2.launder();
+        using PZ = MxEnd<K, INV2, false>;
+        auto wb = [&](auto kc, auto& u) {
+            constexpr int k = decltype(kc)::value, NB = PZ::E / PZ::R;
+            static_for<PZ::R>([&](auto rc) {
+                constexpr int r = decltype(rc)::value;
+                v[0][k + r * NB] = cv<V>(u[r]);
+            });
+        };
+        mx_from<K, INV2, 1, C>(v, t, tw2, lds, wb);
+    } else {
+        constexpr int T = PlanOf<K>::T;
+        fft_pair<K, INV1, INV2, C>(v, t, tw0, lds, [&](int, int m, C& z) { epi(t + T * m, z); });
+    }
+}
 
 // the plan's twiddle table into LDS (TW_LDS; every thread of the workgroup calls it)
 template <int K, int P, int THREADS, class Tw>
@@ -262,9 +456,16 @@ __global__ void __launch_bounds__((RowGeo<K, LAY>::THREADS), (RowGeo<K, LAY>::MI
     const C* in = reinterpret_cast<const C*>(a.in);
     C* out = reinterpret_cast<C*>(a.out);
     C* xf = reinterpret_cast<C*>(a.x);
-    constexpr int N = PlanOf<K>::N, E = PlanOf<K>::E, T = PlanOf<K>::T;
+    constexpr int N = PlanOf<K>::N, T = PlanOf<K>::T;
     constexpr int RPW = RowGeo<K, LAY>::RPW, LINE = RowGeo<K, LAY>::LINE;
     constexpr bool WV = RowGeo<K, LAY>::WAVE;
+    // slot layouts where the line is loaded and stored: the first pass of the
+    // kernel's first transform and the last pass of its last one (one layout,
+    // E elements on T threads, unless the plan is mixed)
+    constexpr bool INV_FIRST = !(OP == RO_FWD || OP == RO_WARM || OP == RO_GD_INIT);
+    constexpr bool INV_LAST = OP == RO_INV;
+    using LD = MxEnd<K, INV_FIRST, true>;
+    using ST = MxEnd<K, INV_LAST, false>;
     __shared__ C smem[RPW * LINE];
     __shared__ TwPod<C> lds_tw[kTwSlots<K, P>];
     // lane -> (row of the tile, t); LAY_B2 pairs: lanes 4k .. 4k + 3 = (r, 2k), (r, 2k + 1),
@@ -285,8 +486,8 @@ __global__ void __launch_bounds__((RowGeo<K, LAY>::THREADS), (RowGeo<K, LAY>::MI
     const long long pix0 = (long long)row * N;  // row start within the hologram (row-major arrays)
     const long long off = (long long)b * a.holo + pix0;
     const long long hoff = (long long)b * a.holo;
-    // the state: B2, or row-major
-    auto st_at = [&](int m) { return LAY == LAY_B2 ? hoff + b2_index(row, t + T * m, a.H) : off + t + T * m; };
+    // the state at element p of the row: B2, or row-major
+    auto st_at = [&](int p) { return LAY == LAY_B2 ? hoff + b2_index(row, p, a.H) : off + p; };
     if constexpr (OP == RO_GS || OP == RO_GD || OP == RO_GS_MID) {
         if (a.checked && a.iter > a.stop[b]) return;  // stopped earlier: frozen (src/algorithms.py:29,83)
     }
@@ -295,55 +496,61 @@ __global__ void __launch_bounds__((RowGeo<K, LAY>::THREADS), (RowGeo<K, LAY>::MI
     lds.stride = LINE;
     lds.x = LAY == LAY_B2 ? (lrow & 1) << 2 : 0;
     Twiddles<K, C, kTwMode<P>> tw;
-    tw_setup<K, P, RowGeo<K, LAY>::THREADS>(tw, lds_tw, a.pl.tw);
-    auto ain = [&](int m) -> S { return a.ain ? (S)a.ain[pix0 + t + T * m] : (S)1; };
-    C v[1][E];
+    auto ain = [&](int p) -> S { return a.ain ? (S)a.ain[pix0 + p] : (S)1; };
+    C v[1][kEMax<K>];
+    if (LD::T == T || t < LD::T) {
 #pragma unroll
-    for (int m = 0; m < E; ++m) {
-        const long long i = off + t + T * m;
-        if constexpr (OP == RO_WARM) {
-            // numpy: exp(1j * float32 phase) is complex64, then times the float64 a_in
-            const S am = ain(m);
-            if constexpr (P == PREC_F64) {
-                double s, c;
-                sincos((double)a.phase_in[i], &s, &c);
-                v[0][m] = make_double2((double)(float)c * am, (double)(float)s * am);
+        for (int m = 0; m < LD::E; ++m) {
+            const int p = t + LD::T * m;
+            const long long i = off + p;
+            if constexpr (OP == RO_WARM) {
+                // numpy: exp(1j * float32 phase) is complex64, then times the float64 a_in
+                const S am = ain(p);
+                if constexpr (P == PREC_F64) {
+                    double s, c;
+                    sincos((double)a.phase_in[i], &s, &c);
+                    v[0][m] = make_double2((double)(float)c * am, (double)(float)s * am);
+                } else {
+                    float s, c;
+                    sincosf(a.phase_in[i], &s, &c);
+                    v[0][m] = make_float2(c * am, s * am);
+                }
+            } else if constexpr (OP == RO_GD_INIT) {
+                const float2 f = a.field0[i];
+                const C x = mk<C>((S)f.x, (S)f.y);
+                xf[i] = x;
+                v[0][m] = u_rz(x, ain(p));
+            } else if constexpr (OP == RO_FWD || OP == RO_INV) {
+                v[0][m] = in[i];  // lone transforms: row-major input
             } else {
-                float s, c;
-                sincosf(a.phase_in[i], &s, &c);
-                v[0][m] = make_float2(c * am, s * am);
+                v[0][m] = in[st_at(p)];
             }
-        } else if constexpr (OP == RO_GD_INIT) {
-            const float2 f = a.field0[i];
-            const C x = mk<C>((S)f.x, (S)f.y);
-            xf[i] = x;
-            v[0][m] = u_rz(x, ain(m));
-        } else if constexpr (OP == RO_FWD || OP == RO_INV) {
-            v[0][m] = in[i];  // lone transforms: row-major input
-        } else {
-            v[0][m] = in[st_at(m)];
         }
     }
+    // the LDS twiddle copy behind the line's loads: its global loads and the
+    // line's are in flight together (a 1080-point complex64 column tile copies
+    // 17 KB of both pass orders)
+    tw_setup<K, P, RowGeo<K, LAY>::THREADS>(tw, lds_tw, a.pl.tw);
     if constexpr (OP == RO_FWD || OP == RO_WARM || OP == RO_GD_INIT) {
-        fft_line<K, false, C>(v, t, tw, lds);
+        rz_line<K, false, C>(v, t, tw, lds);
     } else if constexpr (OP == RO_INV) {
-        fft_line<K, true, C>(v, t, tw, lds);
+        rz_line<K, true, C>(v, t, tw, lds);
     } else if constexpr (OP == RO_COLD) {
         // A0 = ifft2(sqrt T) is complex64 (src/algorithms.py:27); B = a_in A0/|A0| (:30)
-        fft_pair<K, true, false, C>(v, t, tw, lds, [&](int, int m, C& z) { z = unit_rz(round_c64(z), ain(m)); });
+        rz_pair<K, true, false, C>(v, t, tw, lds, [&](int p, C& z) { z = unit_rz(round_c64(z), ain(p)); });
     } else if constexpr (OP == RO_GS) {
         if (a.last || (a.checked && a.stop[b] == a.iter)) {  // uniform per workgroup
-            fft_line_epi<K, true, C>(v, t, tw, lds, [&](int, int m, C& z) {
-                a.phase_out[off + t + T * m] = (float)atan2(z.y, z.x);  // hologram = np.angle(A) (:48)
+            rz_line_epi<K, true, C>(v, t, tw, lds, [&](int p, C& z) {
+                a.phase_out[off + p] = (float)atan2(z.y, z.x);  // hologram = np.angle(A) (:48)
             });
             return;
         }
-        fft_pair<K, true, false, C>(v, t, tw, lds, [&](int, int m, C& z) { z = unit_rz(z, ain(m)); });
+        rz_pair<K, true, false, C>(v, t, tw, lds, [&](int p, C& z) { z = unit_rz(z, ain(p)); });
     } else if constexpr (OP == RO_GS_MID) {
-        fft_pair<K, true, false, C>(v, t, tw, lds, [&](int, int m, C& z) { z = unit_rz(z, ain(m)); });
+        rz_pair<K, true, false, C>(v, t, tw, lds, [&](int p, C& z) { z = unit_rz(z, ain(p)); });
     } else if constexpr (OP == RO_GD_FOURIER) {
         // angle of the complex64 ifft2 is float32, exp of it complex64 (:153-156)
-        fft_pair<K, true, false, C>(v, t, tw, lds, [&](int, int m, C& z) {
+        rz_pair<K, true, false, C>(v, t, tw, lds, [&](int p, C& z) {
             const C c = round_c64(z);
             const float ang = atan2f((float)c.y, (float)c.x);
             float sn, cs;
@@ -354,20 +561,20 @@ __global__ void __launch_bounds__((RowGeo<K, LAY>::THREADS), (RowGeo<K, LAY>::MI
                 sn = (float)s;
                 cs = (float)co;
             }
-            const S am = ain(m);
+            const S am = ain(p);
             const C x = mk<C>((S)cs * am, (S)sn * am);
-            xf[off + t + T * m] = x;
+            xf[off + p] = x;
             z = u_rz(x, am);
         });
     } else if constexpr (OP == RO_GD) {
         // dEdF = ifft2(G) a_in (unscaled transform * 1/S), dEdX_complex, x -= lr dEdX
         // (:87-91, :179-185); next forward input u = a_in x/|x| (:84)
         const S l = (S)a.lr[a.iter];
-        auto update = [&](int m, const C& z) -> C {
-            const S am = ain(m);
+        auto update = [&](int p, const C& z) -> C {
+            const S am = ain(p);
             const S s = am * (S)a.inv_s;
             const S gx = z.x * s, gy = z.y * s;
-            const long long i = off + t + T * m;
+            const long long i = off + p;
             C x = xf[i];
             // dEdX_complex = (g - x Re(conj(x) g) / |x|^2) / |x| (:179-185)
             const S inv = rsq_nr(x.x * x.x + x.y * x.y);
@@ -379,13 +586,15 @@ __global__ void __launch_bounds__((RowGeo<K, LAY>::THREADS), (RowGeo<K, LAY>::MI
             return x;
         };
         if (a.last) {  // the run's last update needs no next forward transform
-            fft_line_epi<K, true, C>(v, t, tw, lds, [&](int, int m, C& z) { (void)update(m, z); });
+            rz_line_epi<K, true, C>(v, t, tw, lds, [&](int p, C& z) { (void)update(p, z); });
             return;
         }
-        fft_pair<K, true, false, C>(v, t, tw, lds, [&](int, int m, C& z) { z = u_rz(update(m, z), ain(m)); });
+        rz_pair<K, true, false, C>(v, t, tw, lds, [&](int p, C& z) { z = u_rz(update(p, z), ain(p)); });
     }
+    if (ST::T == T || t < ST::T) {
 #pragma unroll
-    for (int m = 0; m < E; ++m) out[st_at(m)] = v[0][m];
+        for (int m = 0; m < ST::E; ++m) out[st_at(t + ST::T * m)] = v[0][m];
+    }
 }
 
 template <int K, int CW, int OP, int LAY, int P>
@@ -395,9 +604,14 @@ __global__ void __launch_bounds__((ColGeo<K, CW, P>::THREADS), 1) rz_col_kernel(
     using namespace mr;
     const C* in = reinterpret_cast<const C*>(a.in);
     C* out = reinterpret_cast<C*>(a.out);
-    constexpr int E = PlanOf<K>::E, T = PlanOf<K>::T;
+    constexpr int T = PlanOf<K>::T;
     constexpr int THREADS = ColGeo<K, CW, P>::THREADS;
     constexpr bool WV = ColGeo<K, CW, P>::WAVE;
+    // load / store slot layouts (rz_row_kernel)
+    constexpr bool INV_FIRST = OP == CO_INV || OP == CO_AMP_INV;
+    constexpr bool INV_LAST = !(OP == CO_FWD || OP == CO_GD_STATS);
+    using LD = MxEnd<K, INV_FIRST, true>;
+    using ST = MxEnd<K, INV_LAST, false>;
     __shared__ C smem[ColGeo<K, CW, P>::SLOTS];
     __shared__ TwPod<C> lds_tw[kTwSlots<K, P>];
     const int c = threadIdx.x % CW, t = threadIdx.x / CW;
@@ -406,60 +620,61 @@ __global__ void __launch_bounds__((ColGeo<K, CW, P>::THREADS), 1) rz_col_kernel(
     const int tile = id - b * a.nwg;
     const int col = tile * CW + c;
     const long long hoff = (long long)b * a.holo;
-    const long long base = hoff + (long long)t * a.W + col;  // row-major: row t, this column
-    const long long rstep = (long long)T * a.W;              // slot m: + m rstep
-    const long long bbase = hoff + b2_index(t, col, a.H);    // B2 (target copy, LAY_B2 state): slot m: + 2 T m
-    auto st_at = [&](int m) { return LAY == LAY_B2 ? bbase + 2LL * T * m : base + m * rstep; };
+    const long long cbase = hoff + col;                  // row-major: element p of this column at + p W
+    const long long bbase = hoff + b2_index(0, col, a.H);  // B2 (target copy, LAY_B2 state): + 2 p
+    auto rm_at = [&](int p) { return cbase + (long long)p * a.W; };
+    auto st_at = [&](int p) { return LAY == LAY_B2 ? bbase + 2LL * p : rm_at(p); };
     // the target: the B2 float copy (LAY_B2), else as uploaded (row-major; on LAY_RM the
     // copy measured slower, 4096^2 column pass 289 -> 325 us, profiles/r06)
-    auto tgt_val = [&](int m, int tt) -> float {
-        return LAY == LAY_B2 ? a.tgt_blk[bbase + 2LL * T * m] : tgt_at(a.tgt, tt, base + m * rstep);
+    auto tgt_val = [&](int p, int tt) -> float {
+        return LAY == LAY_B2 ? a.tgt_blk[bbase + 2LL * p] : tgt_at(a.tgt, tt, rm_at(p));
     };
     if constexpr (OP == CO_GS || OP == CO_GD_STATS || OP == CO_GD_GRAD || OP == CO_GD_GRAD_U8) {
         if (a.checked && a.iter > a.stop[b]) return;  // stopped earlier: frozen
     }
     const LdsTile<CW, C, 0, WV> lds{smem, c};
     Twiddles<K, C, kTwMode<P>> tw;
-    tw_setup<K, P, THREADS>(tw, lds_tw, a.pl.tw);
-    C v[1][E];
+    C v[1][kEMax<K>];
+    if (LD::T == T || t < LD::T) {
 #pragma unroll
-    for (int m = 0; m < E; ++m) {
-        if constexpr (OP == CO_AMP_INV)
-            v[0][m] = mk<C>(amp_rz<S>(tgt_val(m, a.tt), a.tt), (S)0);
-        else
-            v[0][m] = in[st_at(m)];
+        for (int m = 0; m < LD::E; ++m) {
+            const int p = t + LD::T * m;
+            if constexpr (OP == CO_AMP_INV)
+                v[0][m] = mk<C>(amp_rz<S>(tgt_val(p, a.tt), a.tt), (S)0);
+            else
+                v[0][m] = in[st_at(p)];
+        }
     }
+    tw_setup<K, P, THREADS>(tw, lds_tw, a.pl.tw);  // behind the line's loads (rz_row_kernel)
     if constexpr (OP == CO_FWD) {
-        fft_line<K, false, C>(v, t, tw, lds);
+        rz_line<K, false, C>(v, t, tw, lds);
     } else if constexpr (OP == CO_INV || OP == CO_AMP_INV) {
-        fft_line<K, true, C>(v, t, tw, lds);
+        rz_line<K, true, C>(v, t, tw, lds);
     } else {
         double mx = 0.0, s2 = 0.0, st = 0.0;
-        auto stats = [&](int m, const C& z, float tv) -> double {
-            const long long i = base + m * rstep;
+        auto stats = [&](int p, const C& z, float tv) -> double {
             const double en = (double)(z.x * z.x + z.y * z.y);
             mx = fmax(mx, en);
             s2 += en * en;
             st += en * (double)tv;
-            if (a.write_e) a.e_out[i] = (float)en;
+            if (a.write_e) a.e_out[rm_at(p)] = (float)en;
             return en;
         };
         if constexpr (OP == CO_GS) {
             // E = |C|^2 statistics and expected output, D = a_T C/|C| (:33,36-38)
-            fft_pair<K, false, true, C>(v, t, tw, lds, [&](int, int m, C& z) {
-                const float tv = tgt_val(m, a.tt);
-                (void)stats(m, z, tv);
+            rz_pair<K, false, true, C>(v, t, tw, lds, [&](int p, C& z) {
+                const float tv = tgt_val(p, a.tt);
+                (void)stats(p, z, tv);
                 z = unit_rz(z, amp_rz<S>(tv, a.tt));
             });
         } else if constexpr (OP == CO_GD_STATS) {
-            fft_line_epi<K, false, C>(v, t, tw, lds,
-                                      [&](int, int m, C& z) { (void)stats(m, z, tgt_val(m, a.tt)); });
+            rz_line_epi<K, false, C>(v, t, tw, lds, [&](int p, C& z) { (void)stats(p, z, tgt_val(p, a.tt)); });
         } else if constexpr (OP == CO_GD_GRAD || OP == CO_GD_GRAD_U8) {
             // G = mask F (s P - T), s = norm / max P (:80,85-88); numpy's mask dtype:
             // float32 for a float32 target, float64 for uint8
             const S s = (S)(a.norm[b] / a.stats[((long long)b * a.max_loops + a.iter) * 4]);
-            fft_pair<K, false, true, C>(v, t, tw, lds, [&](int, int m, C& z) {
-                const S tv = (S)tgt_val(m, OP == CO_GD_GRAD_U8 ? TGT_U8 : TGT_F32);
+            rz_pair<K, false, true, C>(v, t, tw, lds, [&](int p, C& z) {
+                const S tv = (S)tgt_val(p, OP == CO_GD_GRAD_U8 ? TGT_U8 : TGT_F32);
                 const S mask = OP == CO_GD_GRAD_U8
                                    ? (S)(1.0 + (double)a.wa * (double)tv / 255.0)
                                    : (S)(1.0f + __fdiv_rn(__fmul_rn(a.wa, (float)tv), 255.0f));
@@ -479,12 +694,15 @@ __global__ void __launch_bounds__((ColGeo<K, CW, P>::THREADS), 1) rz_col_kernel(
         }
         if constexpr (OP == CO_GD_STATS) return;
     }
+    if (ST::T == T || t < ST::T) {
 #pragma unroll
-    for (int m = 0; m < E; ++m) {
-        if constexpr (OP == CO_FWD || OP == CO_INV)
-            out[base + m * rstep] = v[0][m];  // lone transforms: row-major output
-        else
-            out[st_at(m)] = v[0][m];
+        for (int m = 0; m < ST::E; ++m) {
+            const int p = t + ST::T * m;
+            if constexpr (OP == CO_FWD || OP == CO_INV)
+                out[rm_at(p)] = v[0][m];  // lone transforms: row-major output
+            else
+                out[st_at(p)] = v[0][m];
+        }
     }
 }
 
@@ -519,10 +737,11 @@ SLM_RZ_DECLARE(20)
 SLM_RZ_DECLARE(21)
 SLM_RZ_DECLARE(22)
 SLM_RZ_DECLARE(23)
+SLM_RZ_DECLARE(24)
 #undef SLM_RZ_DECLARE
 #define SLM_RZ_FOR_EACH_KEY(X) \
     X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) X(17) X(18) X(19) X(20) \
-    X(21) X(22) X(23)
+    X(21) X(22) X(23) X(24)
 
 // launch op on plan key k (0 on success, -1 on a launch error or an unbuilt key)
 inline int rz_row_launch(int k, int prec, int lay, int op, const mr::RowArgs& a, int grid, hipStream_t st) {

@@ -19,7 +19,7 @@ import pytest
 from oracle import gs_gd_oracle as orc
 
 PHASE_RMS_TOL = 1e-5
-PANELS = [(1080, 1920), (1200, 1920), (600, 800), (1000, 1024), (768, 1280), (1152, 1536)]
+PANELS = [(1080, 1920), (1920, 1080), (1200, 1920), (600, 800), (1000, 1024), (768, 1280), (1152, 1536)]
 
 
 @pytest.fixture
@@ -84,8 +84,8 @@ def test_c64_fft2_vs_numpy(gpu, c64_engine, shape):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shape,iters", [((1080, 1920), 100), ((600, 800), 200), ((1000, 1024), 200),
-                                         ((1152, 1536), 100)])
+@pytest.mark.parametrize("shape,iters", [((1080, 1920), 100), ((1920, 1080), 100), ((600, 800), 200),
+                                         ((1000, 1024), 200), ((1152, 1536), 100)])
 def test_c64_gs_warm_start_vs_oracle(gpu, c64_engine, shape, iters):
     """SURVEY.md 8c warm-start protocol against the faithful float64 oracle:
     the float32 engine's bar (1e-5 rms), error curve and expected output."""
