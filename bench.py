@@ -569,7 +569,7 @@ def main():
         extra = {"pcie_inclusive": pcie_inclusive(plan, targets(0, bper, n), iters)}
         try:  # every line at its BASELINE.json config's own iteration count
             extra["gs_256_it50"] = secondary(256, 1, 50, reps=20)  # configs[0]'s workload on the GPU
-            # a 1080 x 1920 SLM panel (no float32 radix plan): the float64 mixed-radix engine
+            # a 1080 x 1920 SLM panel (13-smooth sides): the complex64 mixed-plan radix kernels
             extra["gs_1080x1920"] = secondary(1080, 1, 200, width=1920, reps=2)
             extra["gs_4096"] = secondary(4096, 1, 200)  # north-star shape, one hologram
             extra["gs_4096_batch8"] = secondary(4096, 8, 200)  # configs[4] per GPU at 8 GPUs

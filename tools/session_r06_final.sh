@@ -22,5 +22,5 @@ cd /tmp && export TMPDIR=/tmp && cd $repo
 B="bench.py --steps 5 --warmup 1 --no-extra --no-cpu-baseline"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace -o trace -- python3 $B > $out/trace.log 2>&1 || { echo "trace failed rc=$?"; tail -20 $out/trace.log; exit 1; }
 python3 tools/frac_check.py $out/trace/trace_kernel_trace.csv $out/bench.json --source $tag > $out/frac_check.txt 2>&1; cat $out/frac_check.txt | tail -5
-timeout -k 10 1200 bash tools/pmc_configs.sh ${tag}_pmc gs:1024:1:200:f32 gs:4096:1:200:f32 gs:4096:8:200:f32 gs:1024:64:200:f32 gd:1024:1:500:f32 gs:4096:1:200:f64:c128 gd:1024:1:500:f64:c128 > $out/pmc.txt 2>&1 || { echo "pmc failed"; tail -20 $out/pmc.txt; exit 1; }
+timeout -k 10 1200 bash tools/pmc_configs.sh ${tag}_pmc gs:1024:1:200:f32 gs:4096:1:200:f32 gs:4096:8:200:f32 gs:1024:64:200:f32 gd:1024:1:500:f32 gs:4096:1:200:f64:c128 gd:1024:1:500:f64:c128 gs:1080x1920:1:200:f32:radix-c64 > $out/pmc.txt 2>&1 || { echo "pmc failed"; tail -20 $out/pmc.txt; exit 1; }
 echo "done $tag"
