@@ -21,14 +21,14 @@ Engines and the cost model (see DESIGN.md sections 1, 3 and 5):
 * $SLM_ENGINE=float64 on such sides: the complex128 radix-plan kernels
   (complex128 state, float64 arithmetic, the reference's own dtypes; GS
   4096^2 ~0.5 ms, GD 1024^2 ~0.05 ms per iteration);
-* float32 GS targets on 13-smooth SLM panel sides (600, 800, 1000, 1080,
-  1152, 1200, 1280, 1536, 1920, and 2^k / 768 on the other axis): the
-  complex64 radix kernels, the float32 engine's numerics on mixed-E Stockham
-  plans (GS 1080 x 1920: ~0.048 ms per iteration);
-* any other shape whose sides factor into 2, 3, 5, 7, 11, 13 (and uint8 / GD /
-  float64 runs on the panel sides): the float64 mixed-radix kernels,
-  complex128 state, two launches per iteration (GS 1080 x 1920: ~0.08 ms per
-  iteration);
+* 13-smooth SLM panel sides (600, 800, 1000, 1080, 1152, 1200, 1280, 1536,
+  1920, and 2^k / 768 on the other axis): the radix kernels on mixed-E
+  Stockham plans -- float32 GS targets in complex64 with the float32 engine's
+  numerics (GS 1080 x 1920: ~0.048 ms per iteration), uint8 GS, GD and
+  float64 runs in complex128 (GS ~0.070, GD ~0.088 ms);
+* any other shape whose sides factor into 2, 3, 5, 7, 11, 13: the float64
+  mixed-radix kernels, complex128 state, two launches per iteration (~0.08 ms
+  per iteration at 2 Mpixel);
 * a side with a larger prime factor (97, 1272 = 8 * 3 * 53, ...): float64
   1-D line transforms along rows and transposed columns, Bluestein's chirp-z
   for that side -- O(N log N), several launches per transform.

@@ -693,7 +693,7 @@ int rz_cw_of(int ckey, int W, int prec) {
     const int T = kPlans[ckey].n / kPlans[ckey].e;
     // complex64 lines of 64+ threads: 2 (1080 x 1920 column pass 35.4 -> 25.4 us,
     // 768 x 1280 18.7 -> 16.7 us with 4 -> 2 columns, profiles/r06/speed_c64_cw2_p.txt)
-    int cw = T >= (prec == PREC_F32 ? 64 : 128) ? 2 : T >= 16 ? 4 : 8;
+    int cw = T >= (prec == PREC_F32 || kPlans[ckey].variant >= 3 ? 64 : 128) ? 2 : T >= 16 ? 4 : 8;
     if (const char* e = std::getenv("SLM_RZ_CW")) cw = std::atoi(e);
     if (cw < 1 || W % cw || !rz::rz_col_ok(ckey, prec, cw)) return 0;
     return cw;
@@ -728,6 +728,7 @@ bool rz_shape(int B, int H, int W, RzChoice* c, int algo, int prec) {
     if (c->rkey < 0 || c->ckey < 0) return false;
     c->cw = rz_cw_of(c->ckey, W, prec);
     c->lay = rz_layout(algo, H, W, prec);
+    if (rz::key_panel(c->rkey) || rz::key_panel(c->ckey)) c->lay = rz::LAY_B2;  // panel keys: B2 only
     const int rpw = rz::rz_row_rpw(c->rkey, c->lay);
     return c->cw > 0 && rpw > 0 && H % rpw == 0 && W % 2 == 0;  // B2 panels (and the target copy)
 }

@@ -42,14 +42,21 @@ namespace rz {
 // sides); PREC_F32 -- complex64 state, float32 butterflies and projections,
 // complex64 exchanges, the float32 engine's numerics (GS on 13-smooth SLM
 // panel sides by default: plans.hpp variant 3, e.g. 1080 x 1920).
-// Plan keys built per precision: float64 every plan with E <= 16 outside the
-// panel plans (E = 24 / 32 double2 would not fit the register file next to
-// the exchange); float32 every plan with E <= 30 (the panel plans need a
-// multiple of 15 elements per thread).
-__host__ __device__ constexpr bool key_built(int k, int p = PREC_F64) {
-    return k >= 0 && k < kNumPlans &&
-           (p == PREC_F64 ? kPlans[k].e <= 16 && kPlans[k].variant < 3 : kPlans[k].e <= 30);
+// Plan keys built per precision: float64 every plan with at most 16 elements
+// per thread in any pass (E = 24 / 32 double2 would not fit the register file
+// next to the exchange), the panel plans included (GD and uint8 GS on SLM
+// panels); float32 every plan with E <= 30.
+__host__ __device__ constexpr int plan_emax(int k) {  // register slots of a line (mixed plans: the largest ep)
+    int e = kPlans[k].e;
+    if (plan_mixed(k))
+        for (int q = 0; q < kPlans[k].npass; ++q) e = kPlans[k].ep[q] > e ? kPlans[k].ep[q] : e;
+    return e;
 }
+__host__ __device__ constexpr bool key_built(int k, int p = PREC_F64) {
+    return k >= 0 && k < kNumPlans && (p == PREC_F64 ? plan_emax(k) <= 16 : kPlans[k].e <= 30);
+}
+// 13-smooth panel keys (plans.hpp variants 3 / 4): built on the B2 layout only
+__host__ __device__ constexpr bool key_panel(int k) { return k >= 0 && k < kNumPlans && kPlans[k].variant >= 3; }
 
 // Element-wise float64 pieces of these kernels: the reference's exp(i angle z)
 // and z / |z| as z times a refined reciprocal square root (v_rsq_f64 and one
@@ -267,14 +274,7 @@ template <int K, bool INV, bool FIRST>
 using MxEnd = MxPass<K, INV, FIRST ? 0 : kPlans[K].npass - 1>;
 // register slots a kernel's line array needs
 template <int K>
-constexpr int mx_emax() {
-    int e = kPlans[K].e;
-    if (plan_mixed(K))
-        for (int q = 0; q < kPlans[K].npass; ++q) e = kPlans[K].ep[q] > e ? kPlans[K].ep[q] : e;
-    return e;
-}
-template <int K>
-constexpr int kEMax = mx_emax<K>();
+constexpr int kEMax = plan_emax(K);
 
 template <int K, bool INV, int P, class C, class V, int EM, class Lds, class Tw, class Sink>
 __device__ __forceinline__ void mx_from(V (&v)[1][EM], int t, const Tw& tw, const Lds& lds, Sink& sink) {

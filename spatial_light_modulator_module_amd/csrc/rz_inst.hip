@@ -16,16 +16,18 @@ namespace {
 
 static_assert(key_built(SLM_N, PREC_F64) || key_built(SLM_N, PREC_F32), "plan key without radix kernels");
 constexpr bool kF64 = key_built(SLM_N, PREC_F64), kF32 = key_built(SLM_N, PREC_F32);
+constexpr bool kPanel = key_panel(SLM_N);  // panel keys: B2 only at either precision
 
 // the complex64 kernels run GS only (generic.hip rz_shape) on 2- and 4-column tiles (rz_cw_of)
 template <int P>
 constexpr bool row_op_built(int op) {
     return P == PREC_F64 || !(op == mr::RO_GD_FOURIER || op == mr::RO_GD_INIT || op == mr::RO_GD);
 }
+// (panel keys at float64: 2- and 4-column tiles, every op)
 template <int P>
 constexpr bool col_op_built(int op, int cw) {
-    return P == PREC_F64 ||
-           ((cw == 2 || cw == 4) && !(op == mr::CO_GD_STATS || op == mr::CO_GD_GRAD || op == mr::CO_GD_GRAD_U8));
+    if constexpr (P == PREC_F64) return !key_panel(SLM_N) || cw == 2 || cw == 4;
+    return (cw == 2 || cw == 4) && !(op == mr::CO_GD_STATS || op == mr::CO_GD_GRAD || op == mr::CO_GD_GRAD_U8);
 }
 
 template <int CW, int OP, int LAY, int P>
@@ -94,7 +96,7 @@ int col_lay(int cw, int op, const mr::ColArgs& a, int grid, hipStream_t st) {
 
 }  // namespace
 
-// float64: both layouts; float32 (the panel shapes' GS): B2 only
+// float64: both layouts (panel keys: B2); float32 (the panel shapes' GS): B2 only
 int SLM_PASTE(rz_row_launch_, SLM_N)(int prec, int lay, int op, const mr::RowArgs& a, int grid, hipStream_t st) {
     if (prec == PREC_F32) {
         if constexpr (kF32) {
@@ -102,7 +104,11 @@ int SLM_PASTE(rz_row_launch_, SLM_N)(int prec, int lay, int op, const mr::RowArg
         }
         return -1;
     }
-    if constexpr (kF64) return lay == LAY_B2 ? row_lay<LAY_B2, PREC_F64>(op, a, grid, st) : row_lay<LAY_RM, PREC_F64>(op, a, grid, st);
+    if constexpr (kF64 && kPanel) {
+        if (lay == LAY_B2) return row_lay<LAY_B2, PREC_F64>(op, a, grid, st);
+    } else if constexpr (kF64) {
+        return lay == LAY_B2 ? row_lay<LAY_B2, PREC_F64>(op, a, grid, st) : row_lay<LAY_RM, PREC_F64>(op, a, grid, st);
+    }
     return -1;
 }
 
@@ -113,8 +119,11 @@ int SLM_PASTE(rz_col_launch_, SLM_N)(int prec, int lay, int cw, int op, const mr
         }
         return -1;
     }
-    if constexpr (kF64)
+    if constexpr (kF64 && kPanel) {
+        if (lay == LAY_B2) return col_lay<LAY_B2, PREC_F64>(cw, op, a, grid, st);
+    } else if constexpr (kF64) {
         return lay == LAY_B2 ? col_lay<LAY_B2, PREC_F64>(cw, op, a, grid, st) : col_lay<LAY_RM, PREC_F64>(cw, op, a, grid, st);
+    }
     return -1;
 }
 
@@ -126,10 +135,10 @@ int SLM_PASTE(rz_col_ok_, SLM_N)(int prec, int cw) {
     if (!(prec == PREC_F32 ? kF32 : kF64)) return 0;
     const bool f32 = prec == PREC_F32;
     switch (cw) {
-        case 1: return f32 ? 0 : ColGeo<SLM_N, 1>::kValid;
+        case 1: return f32 || kPanel ? 0 : ColGeo<SLM_N, 1>::kValid;
         case 2: return f32 ? ColGeo<SLM_N, 2, PREC_F32>::kValid : ColGeo<SLM_N, 2>::kValid;
         case 4: return f32 ? ColGeo<SLM_N, 4, PREC_F32>::kValid : ColGeo<SLM_N, 4>::kValid;
-        case 8: return f32 ? 0 : ColGeo<SLM_N, 8>::kValid;
+        case 8: return f32 || kPanel ? 0 : ColGeo<SLM_N, 8>::kValid;
         default: return 0;
     }
 }

@@ -45,7 +45,8 @@ def _gs(lib, t, loops, phase=None, tol=0.0, checked=False, want="radix-c128"):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shape", [(64, 64), (128, 256), (768, 1024), (1024, 1024), (256, 2048), (4096, 512)])
+@pytest.mark.parametrize("shape", [(64, 64), (128, 256), (768, 1024), (1024, 1024), (256, 2048), (4096, 512),
+                                   (1080, 1920), (1920, 1080), (600, 800), (1200, 1280), (1000, 1536), (1152, 1152)])
 def test_rz_fft2_c128_vs_numpy(gpu, f64_engine, shape):
     """slm_fft2_c128 on the radix-plan kernels (every plan key the engine
     picks at these shapes) against numpy.fft at float64 accuracy."""
@@ -59,7 +60,7 @@ def test_rz_fft2_c128_vs_numpy(gpu, f64_engine, shape):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shape", [(128, 256), (768, 1024), (1024, 1024)])
+@pytest.mark.parametrize("shape", [(128, 256), (768, 1024), (1024, 1024), (600, 800), (1080, 1920)])
 @pytest.mark.parametrize("u8", [False, True])
 def test_rz_gs_warm_start_vs_oracle(gpu, f64_engine, shape, u8):
     """SURVEY.md 8c warm-start protocol (the oracle's phase after 30 cold
@@ -218,3 +219,33 @@ def test_rz_incoming_amplitude(gpu, f64_engine):
                                                        initial_field=x0)
     assert orc.phase_rms(ph[0], ref) < 1e-5
     np.testing.assert_allclose(errs[0], ref_err, rtol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("guess", ["random", "fourier"])
+def test_rz_gd_panel_vs_oracle(gpu, monkeypatch, guess):
+    """GD on a 13-smooth SLM panel (600 x 800: mixed plans 10.6.10 / 10.8.10 at
+    float64, the default GD engine there) against the faithful float64 oracle,
+    from the host-set random guess and from the device-formed "fourier" guess
+    (chaotic like GS's cold start: first errors pointwise, the last in a band)."""
+    monkeypatch.delenv("SLM_ENGINE", raising=False)
+    monkeypatch.delenv("SLM_GENERIC_ENGINE", raising=False)
+    from spatial_light_modulator_module_amd import algorithms as alg
+
+    shape = (600, 800)
+    t = _target(shape, False, seed=9)
+    loops = 20
+    x0 = alg.make_initial_guess("random", None, t, 42) if guess == "random" else None
+    kw = {"initial_field": x0} if guess == "random" else {"initial_guess": "fourier"}
+    ref, _, ref_err, _ = orc.gradient_descent_faithful(t, loops, 0.005, 1.0, 0, **kw)
+    eng, ph, err = _gd_run(gpu, t, loops, x0)
+    assert eng == ("radix-c128", "radix-c128"), eng
+    rms = orc.phase_rms(ph, ref)
+    print(f"[parity] radix-c128 GD {shape} {guess} guess, {loops} iterations: phase rms {rms:.3e}; "
+          f"final error {err[-1]:.6e} (oracle {ref_err[-1]:.6e})")
+    if guess == "random":
+        assert rms < 1e-5  # the field crosses the C-ABI as complex64
+        np.testing.assert_allclose(err, ref_err, rtol=1e-5)
+    else:
+        np.testing.assert_allclose(err[:3], ref_err[:3], rtol=1e-6)
+        assert 0.5 < err[-1] / ref_err[-1] < 2.0

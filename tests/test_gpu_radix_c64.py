@@ -8,8 +8,8 @@ Stockham radix kernels instead of the float64 mixed radix.
 
 The float32 engine's bar applies (warm start from the oracle's
 30-iteration phase, phase rms <= 1e-5 against the faithful float64 oracle);
-uint8 targets, $SLM_ENGINE=float64 and slm_plan_set_precision(F64) keep the
-float64 mixed radix (tests/test_gpu_generic.py holds that engine to 1e-6).
+uint8 targets, GD, $SLM_ENGINE=float64 and slm_plan_set_precision(F64) run
+the same plans at float64 (tests/test_gpu_radix_c128.py holds them to 1e-6).
 """
 import os
 
@@ -50,19 +50,24 @@ def _workers():
 @pytest.mark.parametrize("shape", PANELS)
 def test_c64_engine_selection(gpu, c64_engine, monkeypatch, shape):
     """float32 GS on a panel shape runs the complex64 radix kernels; uint8,
-    $SLM_ENGINE=float64 and an explicit float64 precision keep float64."""
+    GD, $SLM_ENGINE=float64 and an explicit float64 precision run the same
+    mixed plans at float64 (complex128 state); $SLM_GENERIC_ENGINE=mr the
+    float64 mixed radix."""
     h, w = shape
     with gpu.Plan(gpu.ALGO_GS, 1, h, w, gpu.TGT_F32, False, 2) as p:
         assert p.engine() == ("radix-c64", "radix-c64") and p.info()["precision"] == "f32"
         p.set_precision(gpu.PRECISION_F64)
-        assert p.engine() == ("mixed-radix", "mixed-radix") and p.info()["precision"] == "f64"
+        assert p.engine() == ("radix-c128", "radix-c128") and p.info()["precision"] == "f64"
         p.set_precision(gpu.PRECISION_F32)
         assert p.engine() == ("radix-c64", "radix-c64")
     with gpu.Plan(gpu.ALGO_GS, 1, h, w, gpu.TGT_U8, False, 2) as p:
-        assert p.engine() == ("mixed-radix", "mixed-radix") and p.info()["precision"] == "f64"
+        assert p.engine() == ("radix-c128", "radix-c128") and p.info()["precision"] == "f64"
     with gpu.Plan(gpu.ALGO_GD, 1, h, w, gpu.TGT_F32, False, 2) as p:
-        assert p.engine() == ("mixed-radix", "mixed-radix")
+        assert p.engine() == ("radix-c128", "radix-c128")
     monkeypatch.setenv("SLM_ENGINE", "float64")
+    with gpu.Plan(gpu.ALGO_GS, 1, h, w, gpu.TGT_F32, False, 2) as p:
+        assert p.engine() == ("radix-c128", "radix-c128")
+    monkeypatch.setenv("SLM_GENERIC_ENGINE", "mr")
     with gpu.Plan(gpu.ALGO_GS, 1, h, w, gpu.TGT_F32, False, 2) as p:
         assert p.engine() == ("mixed-radix", "mixed-radix")
 
@@ -112,8 +117,8 @@ def test_c64_gs_warm_start_vs_oracle(gpu, c64_engine, shape, iters):
 @pytest.mark.gpu
 def test_c64_matches_float64_engine(gpu, c64_engine):
     """The same warm-started batch on the complex64 radix kernels and on the
-    float64 mixed radix (slm_plan_set_precision): phases within the float32
-    bar of each other, error curves at float32 accuracy."""
+    float64 ones (slm_plan_set_precision): phases within the float32 bar of
+    each other, error curves at float32 accuracy."""
     t = np.stack([_target((600, 800), seed=s) for s in (1, 2)])
     phi = np.random.default_rng(3).uniform(-np.pi, np.pi, t.shape).astype(np.float32)
     out = {}
@@ -125,10 +130,10 @@ def test_c64_matches_float64_engine(gpu, c64_engine):
             p.run(10)
             out[prec] = (p.engine(), p.read())
     (eng32, (ph32, _, st32, _)), (eng64, (ph64, _, st64, _)) = out[gpu.PRECISION_F32], out[gpu.PRECISION_F64]
-    assert eng32[0] == "radix-c64" and eng64[0] == "mixed-radix"
+    assert eng32[0] == "radix-c64" and eng64[0] == "radix-c128"
     for b in range(2):
         rms = orc.phase_rms(ph32[b], ph64[b])
-        print(f"[parity] radix-c64 vs mixed-radix GS 600x800 hologram {b}, 10 iterations: phase rms {rms:.3e}")
+        print(f"[parity] radix-c64 vs radix-c128 GS 600x800 hologram {b}, 10 iterations: phase rms {rms:.3e}")
         assert rms < PHASE_RMS_TOL
     np.testing.assert_allclose(st32[:, :10, 3], st64[:, :10, 3], rtol=1e-5)
 
