@@ -351,10 +351,11 @@ class Plan:
         2..13 kernels, mixed_radix.hpp) or "bluestein" (float64 1-D line
         transforms along rows and transposed columns, Bluestein's chirp-z
         for a side with a larger prime factor, generic.hip), and under
-        $SLM_ENGINE=float64 on 2^k / 768 sides "radix-c128" (float64
+        $SLM_ENGINE=float64 on 2^k / 768 sides, and for uint8 GS / GD /
+        float64 runs on 13-smooth SLM panel sides, "radix-c128" (float64
         Stockham kernels with complex128 state, radix_c128.hpp); float32 GS on
-        13-smooth SLM panel sides (e.g. 1080 x 1920) "radix-c64" (the same
-        kernels with complex64 state and float32 butterflies)."""
+        panel sides (e.g. 1080 x 1920) "radix-c64" (the same kernels with
+        complex64 state and float32 butterflies)."""
         c, r = ctypes.c_int(), ctypes.c_int()
         check(self._lib.slm_plan_engine(self.handle, ctypes.byref(c), ctypes.byref(r)), "slm_plan_engine")
         names = ("stockham", "shuffle", "bluestein", "mixed-radix", "radix-c128", "radix-c64")
