@@ -398,6 +398,18 @@ struct LdsTile {  // CW interleaved columns (column kernels): [o][c]; the thread
         const X v = base[cur + (o + (o >> 4)) * CW + c + l];
         return mk<C>(v.x, v.y);
     }
+    // unpadded slots (radix_c128.hpp mixed plans, exchanges whose writes are
+    // lane-contiguous): the index is linear in o, so the constant part of a
+    // butterfly's R outputs folds into the ds_write / ds_read offset
+    template <class C>
+    __device__ __forceinline__ void store_lin(int l, int o, C v) const {
+        base[cur + o * CW + c + l] = mk<X>(v.x, v.y);
+    }
+    template <class C>
+    __device__ __forceinline__ C load_lin(int l, int o) const {
+        const X v = base[cur + o * CW + c + l];
+        return mk<C>(v.x, v.y);
+    }
 };
 
 

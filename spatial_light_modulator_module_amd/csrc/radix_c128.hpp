@@ -213,6 +213,16 @@ struct LdsPairRow : LdsLine<X, 0, WAVE> {
         const X v = this->base[this->cur + l * this->stride + (lds_slot(o) ^ x)];
         return mk<C>(v.x, v.y);
     }
+    // unswizzled slots (mixed plans, LdsTile::store_lin)
+    template <class C>
+    __device__ __forceinline__ void store_lin(int l, int o, C v) const {
+        this->base[this->cur + l * this->stride + o] = mk<X>(v.x, v.y);
+    }
+    template <class C>
+    __device__ __forceinline__ C load_lin(int l, int o) const {
+        const X v = this->base[this->cur + l * this->stride + o];
+        return mk<C>(v.x, v.y);
+    }
 };
 
 // complex64: table twiddles where used (TW_DIRECT_LAUNDER, L1/L2-resident);
@@ -296,10 +306,18 @@ __device__ __forceinline__ void mx_from(V (&v)[1][EM], int t, const Tw& tw, cons
             if constexpr (Ps::LAST) {
                 sink(kc, u);
             } else {
+                // Only a transform's first pass (Ns = 1) writes at a stride (o = R b + r):
+                // its exchange keeps the bank swizzle / padding. Later passes write runs
+                // of consecutive j, so their exchanges use plain slots, whose index
+                // arithmetic folds into the LDS instruction offsets (the swizzle cost
+                // ~5 VALU per element access, a third of the 1920-point row pass's VALU)
                 const int o = (b / Ns) * Ns * R + j;
                 static_for<R>([&](auto rc) {
                     constexpr int r = decltype(rc)::value;
-                    lds.store(0, o + r * Ns, u[r]);
+                    if constexpr (Ns == 1)
+                        lds.store(0, o + r * Ns, u[r]);
+                    else
+                        lds.store_lin(0, o + r * Ns, u[r]);
                 });
             }
             __builtin_amdgcn_sched_barrier(0);
@@ -311,7 +329,10 @@ __device__ __forceinline__ void mx_from(V (&v)[1][EM], int t, const Tw& tw, cons
         if (Pn::T == kTMax<K> || t < Pn::T) {
             static_for<Pn::E>([&](auto mc) {
                 constexpr int m = decltype(mc)::value;
-                v[0][m] = lds.template load<V>(0, t + m * Pn::T);
+                if constexpr (Ns == 1)
+                    v[0][m] = lds.template load<V>(0, t + m * Pn::T);
+                else
+                    v[0][m] = lds.template load_lin<V>(0, t + m * Pn::T);
             });
         }
         exchange_done(lds);
