@@ -492,6 +492,23 @@ struct Twiddles<N, C, TW_DIRECT> {
             u[r] = INV ? cmulc(u[r], t) : cmul(u[r], t);
         });
     }
+    // the same split in two (radix_c128.hpp mixed plans: a pass's twiddles fetched
+    // before the previous exchange, applied after it)
+    template <int TwOff, int R, int Ns>
+    __device__ __forceinline__ void fetch(C* w, int j) const {
+        static_for<R - 1>([&](auto rc) {
+            constexpr int r = decltype(rc)::value + 1;
+            const int i = TwOff + (r - 1) * Ns + j;
+            w[r - 1] = mk<C>(table[i].x, table[i].y);
+        });
+    }
+    template <int R, bool INV>
+    __device__ __forceinline__ static void apply_fetched(C* u, const C* w) {
+        static_for<R - 1>([&](auto rc) {
+            constexpr int r = decltype(rc)::value + 1;
+            u[r] = INV ? cmulc(u[r], w[r - 1]) : cmul(u[r], w[r - 1]);
+        });
+    }
 };
 // TW_DIRECT whose loads are laundered before every transform whatever E (the
 // complex128 radix-plan kernels: a fused pair's second transform would

@@ -140,6 +140,21 @@ struct Twiddles<N, C, rz::TW_LDS> {
             u[r] = INV ? cmulc(u[r], t) : cmul(u[r], t);
         });
     }
+    template <int TwOff, int R, int Ns>
+    __device__ __forceinline__ void fetch(C* w, int j) const {
+        static_for<R - 1>([&](auto rc) {
+            constexpr int r = decltype(rc)::value + 1;
+            const int i = TwOff + (r - 1) * Ns + j;
+            w[r - 1] = mk<C>(table[i].x, table[i].y);
+        });
+    }
+    template <int R, bool INV>
+    __device__ __forceinline__ static void apply_fetched(C* u, const C* w) {
+        static_for<R - 1>([&](auto rc) {
+            constexpr int r = decltype(rc)::value + 1;
+            u[r] = INV ? cmulc(u[r], w[r - 1]) : cmul(u[r], w[r - 1]);
+        });
+    }
 };
 
 template <int N, class C>
@@ -158,6 +173,20 @@ struct Twiddles<N, C, rz::TW_POW> {
     template <int TwOff, int RegOff, int PowOff, int R, int Ns, bool INV>
     __device__ __forceinline__ void apply(C* u, int, int j) const {
         const C w1 = mk<C>(table[TwOff + j].x, table[TwOff + j].y);  // entry (r - 1) Ns + j at r = 1
+        C w = w1;
+        static_for<R - 1>([&](auto rc) {
+            constexpr int r = decltype(rc)::value + 1;
+            if constexpr (r > 1) w = cmul(w, w1);
+            u[r] = INV ? cmulc(u[r], w) : cmul(u[r], w);
+        });
+    }
+    template <int TwOff, int R, int Ns>
+    __device__ __forceinline__ void fetch(C* w, int j) const {
+        w[0] = mk<C>(table[TwOff + j].x, table[TwOff + j].y);
+    }
+    template <int R, bool INV>
+    __device__ __forceinline__ static void apply_fetched(C* u, const C* wf) {
+        const C w1 = wf[0];
         C w = w1;
         static_for<R - 1>([&](auto rc) {
             constexpr int r = decltype(rc)::value + 1;
@@ -286,8 +315,33 @@ using MxEnd = MxPass<K, INV, FIRST ? 0 : kPlans[K].npass - 1>;
 template <int K>
 constexpr int kEMax = plan_emax(K);
 
-template <int K, bool INV, int P, class C, class V, int EM, class Lds, class Tw, class Sink>
-__device__ __forceinline__ void mx_from(V (&v)[1][EM], int t, const Tw& tw, const Lds& lds, Sink& sink) {
+// A pass's twiddles, fetched before the exchange that precedes the pass (their
+// global / LDS loads then overlap that exchange's writes, barrier and reads
+// instead of stalling the pass's first butterfly) and applied in it: the same
+// values and products as Twiddles::apply.
+template <class C, int NB, int R>
+struct MxTw {
+    C w[NB][R > 1 ? R - 1 : 1];
+};
+template <int K, bool INV, int P, class C, class Tw>
+__device__ __forceinline__ auto mx_fetch(const Tw& tw, int t) {
+    using Ps = MxPass<K, INV, P>;
+    constexpr int R = Ps::R, T = Ps::T, Ns = Ps::NS, NB = Ps::E / R;
+    MxTw<C, NB, R> f;
+    if constexpr (Ns > 1) {
+        if (T == kTMax<K> || t < T) {
+            static_for<NB>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                tw.template fetch<Ps::TWOFF, R, Ns>(f.w[k], (t + k * T) % Ns);
+            });
+        }
+    }
+    return f;
+}
+
+template <int K, bool INV, int P, class C, class V, int EM, class Lds, class Tw, class Sink, class Pre>
+__device__ __forceinline__ void mx_from(V (&v)[1][EM], int t, const Tw& tw, const Lds& lds, Sink& sink,
+                                        const Pre& pre) {
     using Ps = MxPass<K, INV, P>;
     constexpr int R = Ps::R, E = Ps::E, T = Ps::T, Ns = Ps::NS, NB = E / R;
     asm volatile("" : "+v"(t));  // per-pass address arithmetic (stockham_from)
@@ -301,7 +355,7 @@ __device__ __forceinline__ void mx_from(V (&v)[1][EM], int t, const Tw& tw, cons
                 constexpr int r = decltype(rc)::value;
                 u[r] = cv<C>(v[0][k + r * NB]);
             });
-            if constexpr (Ns > 1) tw.template apply<Ps::TWOFF, 0, 0, R, Ns, INV>(u, k, j);
+            if constexpr (Ns > 1) Tw::template apply_fetched<R, INV>(u, pre.w[k]);
             Dft<R, INV, C>::run(u);
             if constexpr (Ps::LAST) {
                 sink(kc, u);
@@ -325,6 +379,7 @@ __device__ __forceinline__ void mx_from(V (&v)[1][EM], int t, const Tw& tw, cons
     }
     if constexpr (!Ps::LAST) {
         using Pn = MxPass<K, INV, P + 1>;
+        const auto nxt = mx_fetch<K, INV, P + 1, C>(tw, t);
         exchange_sync(lds);
         if (Pn::T == kTMax<K> || t < Pn::T) {
             static_for<Pn::E>([&](auto mc) {
@@ -336,7 +391,7 @@ __device__ __forceinline__ void mx_from(V (&v)[1][EM], int t, const Tw& tw, cons
             });
         }
         exchange_done(lds);
-        mx_from<K, INV, P + 1, C>(v, t, tw, lds, sink);
+        mx_from<K, INV, P + 1, C>(v, t, tw, lds, sink, nxt);
     }
 }
 
@@ -356,7 +411,7 @@ __device__ __forceinline__ void rz_line(V (&v)[1][EM], int t, const Tw& tw0, con
                 v[0][k + r * NB] = cv<V>(u[r]);
             });
         };
-        mx_from<K, INV, 0, C>(v, t, tw, lds, wb);
+        mx_from<K, INV, 0, C>(v, t, tw, lds, wb, MxTw<C, 1, 1>{});
     } else {
         fft_line<K, INV, C>(v, t, tw0, lds);
     }
@@ -375,7 +430,7 @@ __device__ __forceinline__ void rz_line_epi(V (&v)[1][EM], int t, const Tw& tw0,
                 v[0][k + r * NB] = cv<V>(u[r]);
             });
         };
-        mx_from<K, INV, 0, C>(v, t, tw, lds, sink);
+        mx_from<K, INV, 0, C>(v, t, tw, lds, sink, MxTw<C, 1, 1>{});
     } else {
         constexpr int T = PlanOf<K>::T;
         fft_line_epi<K, INV, C>(v, t, tw0, lds, [&](int, int m, C& z) { epi(t + T * m, z); });
@@ -403,8 +458,11 @@ __device__ __forceinline__ void rz_pair(V (&v)[1][EM], int t, const Tw& tw0, con
                 lds.store(0, o + r, u[r]);
             });
         };
-        mx_from<K, INV1, 0, C>(v, t, tw, lds, sink);
+        mx_from<K, INV1, 0, C>(v, t, tw, lds, sink, MxTw<C, 1, 1>{});
         using P1 = MxPass<K, INV2, 1>;
+        Tw tw2 = tw0;
+        tw2.launder();
+        const auto nxt = mx_fetch<K, INV2, 1, C>(tw2, t);
         exchange_sync(lds);
         if (P1::T == kTMax<K> || t < P1::T) {
             static_for<P1::E>([&](auto mc) {
@@ -413,8 +471,6 @@ __device__ __forceinline__ void rz_pair(V (&v)[1][EM], int t, const Tw& tw0, con
             });
         }
         exchange_done(lds);
-        Tw tw2 = tw0;
-        tw2.launder();
         using PZ = MxEnd<K, INV2, false>;
         auto wb = [&](auto kc, auto& u) {
             constexpr int k = decltype(kc)::value, NB = PZ::E / PZ::R;
@@ -423,7 +479,7 @@ __device__ __forceinline__ void rz_pair(V (&v)[1][EM], int t, const Tw& tw0, con
                 v[0][k + r * NB] = cv<V>(u[r]);
             });
         };
-        mx_from<K, INV2, 1, C>(v, t, tw2, lds, wb);
+        mx_from<K, INV2, 1, C>(v, t, tw2, lds, wb, nxt);
     } else {
         constexpr int T = PlanOf<K>::T;
         fft_pair<K, INV1, INV2, C>(v, t, tw0, lds, [&](int, int m, C& z) { epi(t + T * m, z); });
