@@ -395,51 +395,46 @@ __device__ __forceinline__ void mx_from(V (&v)[1][EM], int t, const Tw& tw, cons
     }
 }
 
-// Transform wrappers of the radix kernels: epi(p, z) sees each output z with
-// its element position p along the line (single-E plans: fft_core.hpp's
-// drivers, slot m of thread t at p = t + T m; mixed plans: mx_from).
+// Transform wrappers of the radix kernels, on mx_from for every plan (a
+// single-E plan is a mixed plan with one E): epi(p, z) sees each output z with
+// its element position p along the line. Single-E plans ran fft_core.hpp's
+// Stockham driver until r06; mx_from's plain slots after the first pass and
+// fetched-ahead twiddles measured faster on every complex128 / complex64 shape
+// tried (GD 4096^2 0.665 -> 0.640 ms, GD 1024^2 0.0445 -> 0.0415, GS 2048^2
+// 0.094 -> 0.089; profiles/r06/ab_mx_all_zb.txt).
 template <int K, bool INV, class C, class V, int EM, class Lds, class Tw>
 __device__ __forceinline__ void rz_line(V (&v)[1][EM], int t, const Tw& tw0, const Lds& lds) {
-    if constexpr (plan_mixed(K)) {
-        Tw tw = tw0;
-        tw.launder();
-        using PL = MxEnd<K, INV, false>;
-        auto wb = [&](auto kc, auto& u) {
-            constexpr int k = decltype(kc)::value, NB = PL::E / PL::R;
-            static_for<PL::R>([&](auto rc) {
-                constexpr int r = decltype(rc)::value;
-                v[0][k + r * NB] = cv<V>(u[r]);
-            });
-        };
-        mx_from<K, INV, 0, C>(v, t, tw, lds, wb, MxTw<C, 1, 1>{});
-    } else {
-        fft_line<K, INV, C>(v, t, tw0, lds);
-    }
+    Tw tw = tw0;
+    tw.launder();
+    using PL = MxEnd<K, INV, false>;
+    auto wb = [&](auto kc, auto& u) {
+        constexpr int k = decltype(kc)::value, NB = PL::E / PL::R;
+        static_for<PL::R>([&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            v[0][k + r * NB] = cv<V>(u[r]);
+        });
+    };
+    mx_from<K, INV, 0, C>(v, t, tw, lds, wb, MxTw<C, 1, 1>{});
 }
 template <int K, bool INV, class C, class V, int EM, class Lds, class Tw, class Epi>
 __device__ __forceinline__ void rz_line_epi(V (&v)[1][EM], int t, const Tw& tw0, const Lds& lds, Epi&& epi) {
-    if constexpr (plan_mixed(K)) {
-        Tw tw = tw0;
-        tw.launder();
-        using PL = MxEnd<K, INV, false>;
-        auto sink = [&](auto kc, auto& u) {
-            constexpr int k = decltype(kc)::value, NB = PL::E / PL::R;
-            static_for<PL::R>([&](auto rc) {
-                constexpr int r = decltype(rc)::value;
-                epi(t + PL::T * (k + r * NB), u[r]);
-                v[0][k + r * NB] = cv<V>(u[r]);
-            });
-        };
-        mx_from<K, INV, 0, C>(v, t, tw, lds, sink, MxTw<C, 1, 1>{});
-    } else {
-        constexpr int T = PlanOf<K>::T;
-        fft_line_epi<K, INV, C>(v, t, tw0, lds, [&](int, int m, C& z) { epi(t + T * m, z); });
-    }
+    Tw tw = tw0;
+    tw.launder();
+    using PL = MxEnd<K, INV, false>;
+    auto sink = [&](auto kc, auto& u) {
+        constexpr int k = decltype(kc)::value, NB = PL::E / PL::R;
+        static_for<PL::R>([&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            epi(t + PL::T * (k + r * NB), u[r]);
+            v[0][k + r * NB] = cv<V>(u[r]);
+        });
+    };
+    mx_from<K, INV, 0, C>(v, t, tw, lds, sink, MxTw<C, 1, 1>{});
 }
 template <int K, bool INV1, bool INV2, class C, class V, int EM, class Lds, class Tw, class Epi>
 __device__ __forceinline__ void rz_pair(V (&v)[1][EM], int t, const Tw& tw0, const Lds& lds, Epi&& epi) {
-    if constexpr (plan_mixed(K)) {
-        static_assert(INV1 != INV2, "a mixed pair runs one transform forwards and the other backwards");
+    {
+        static_assert(INV1 != INV2, "a pair runs one transform forwards and the other backwards");
         using PL = MxEnd<K, INV1, false>;  // the first transform's last pass ...
         using PF = MxEnd<K, INV2, true>;   // ... is the second one's first (same radix and slots)
         static_assert(PL::R == PF::R && PL::E == PF::E, "mixed pair: passes do not meet");
@@ -480,9 +475,6 @@ __device__ __forceinline__ void rz_pair(V (&v)[1][EM], int t, const Tw& tw0, con
             });
         };
         mx_from<K, INV2, 1, C>(v, t, tw2, lds, wb, nxt);
-    } else {
-        constexpr int T = PlanOf<K>::T;
-        fft_pair<K, INV1, INV2, C>(v, t, tw0, lds, [&](int, int m, C& z) { epi(t + T * m, z); });
     }
 }
 
