@@ -9,12 +9,13 @@
 // (DESIGN.md section 5). The mixed-radix kernels (mixed_radix.hpp) keep
 // complex128 but run one butterfly at a time with runtime radices and table
 // twiddles from L2 (latency-bound, 0.23 of 8 TB/s). These kernels put the
-// float32 engine's structure under complex128 state: the Stockham driver of
-// fft_core.hpp with C = V = X = double2 (float64 butterflies and twiddles,
-// complex128 registers between passes, complex128 LDS exchanges), a whole
-// line per thread group with E elements per thread held in registers, and
-// the element-wise projection between a launch's two transforms running on
-// the last butterfly group still in registers (fft_pair).
+// float32 engine's structure under complex128 state: compile-time Stockham
+// transforms (fft_core.hpp's butterflies, the mixed-plan driver mx_from below)
+// with C = V = X = double2 (float64 butterflies and twiddles, complex128
+// registers between passes, complex128 LDS exchanges), a whole line per thread
+// group with its elements held in registers, and the element-wise projection
+// between a launch's two transforms running on the last butterfly group still
+// in registers (rz_pair).
 //
 // Layout and contract are the mixed-radix back end's (mr::RowArgs /
 // mr::ColArgs, generic.hip): row-major complex128 [B][H][W] state, row-major
@@ -109,53 +110,10 @@ __device__ __forceinline__ S amp_rz(float t, int tt) {
 // 1024-point column pass, profiles/r06/sq_rz1024_d.txt). Loads laundered
 // before every transform (TW_DIRECT_LAUNDER).
 constexpr int TW_POW = 3;
-// Twiddles of the complex64 kernels: every twiddle from the table (float32
-// powers would drift ~1e-6). TW_LDS copies the table into LDS at the kernel's
-// start (it served the single-E panel plans, one wave per SIMD; kept
-// selectable, kTwMode below).
-constexpr int TW_LDS = 4;
-template <class C>
-struct alignas(2 * sizeof(Scalar<C>)) TwPod {  // trivially copyable twin of C
-    Scalar<C> x, y;
-};
+// Twiddles of the complex64 kernels: every twiddle from the table where used
+// (TW_DIRECT_LAUNDER; float32 powers would drift ~1e-6).
 
 }  // namespace rz
-
-template <int N, class C>
-struct Twiddles<N, C, rz::TW_LDS> {
-    static constexpr bool kAlwaysLaunder = true;
-    using LdsPtr = const __attribute__((address_space(3))) rz::TwPod<C>*;
-    LdsPtr table;
-    __device__ __forceinline__ void launder() {  // distinct loads per transform (fft_core.hpp TW_DIRECT)
-        unsigned q = (unsigned)(unsigned long long)table;
-        asm volatile("" : "+s"(q));
-        table = (LdsPtr)(unsigned long long)q;
-    }
-    template <int TwOff, int RegOff, int PowOff, int R, int Ns, bool INV>
-    __device__ __forceinline__ void apply(C* u, int, int j) const {
-        static_for<R - 1>([&](auto rc) {
-            constexpr int r = decltype(rc)::value + 1;
-            const int i = TwOff + (r - 1) * Ns + j;
-            const C t = mk<C>(table[i].x, table[i].y);
-            u[r] = INV ? cmulc(u[r], t) : cmul(u[r], t);
-        });
-    }
-    template <int TwOff, int R, int Ns>
-    __device__ __forceinline__ void fetch(C* w, int j) const {
-        static_for<R - 1>([&](auto rc) {
-            constexpr int r = decltype(rc)::value + 1;
-            const int i = TwOff + (r - 1) * Ns + j;
-            w[r - 1] = mk<C>(table[i].x, table[i].y);
-        });
-    }
-    template <int R, bool INV>
-    __device__ __forceinline__ static void apply_fetched(C* u, const C* w) {
-        static_for<R - 1>([&](auto rc) {
-            constexpr int r = decltype(rc)::value + 1;
-            u[r] = INV ? cmulc(u[r], w[r - 1]) : cmul(u[r], w[r - 1]);
-        });
-    }
-};
 
 template <int N, class C>
 struct Twiddles<N, C, rz::TW_POW> {
@@ -254,16 +212,13 @@ struct LdsPairRow : LdsLine<X, 0, WAVE> {
     }
 };
 
-// complex64: table twiddles where used (TW_DIRECT_LAUNDER, L1/L2-resident);
-// the LDS copy (TW_LDS) measured slower once the mixed plans put 2-4 waves per
-// SIMD on the chip (1920 x 1080 42.5 against 54.4 us per GS iteration: the
-// copy of both pass orders doubled a 1920-point column tile's LDS;
-// profiles/r06/speed_c64_twg_r.txt)
+// complex64: table twiddles where used (TW_DIRECT_LAUNDER, L1/L2-resident); a
+// copy of the table into LDS at the kernel's start (both pass orders of a mixed
+// plan) measured slower once the mixed plans put 2-4 waves per SIMD on the chip
+// (1920 x 1080 42.5 against 54.4 us per GS iteration; profiles/r06/speed_c64_twg_r.txt;
+// removed)
 template <int P>
 constexpr int kTwMode = P == PREC_F64 ? TW_POW : TW_DIRECT_LAUNDER;
-// LDS twiddle slots of a kernel (1: unused; mixed plans hold both pass orders)
-template <int K, int P>
-constexpr int kTwSlots = kTwMode<P> == TW_LDS && twiddle_count_all(K) > 0 ? twiddle_count_all(K) : 1;
 
 // ------------------------------------------------------------------------
 // Mixed plans (plans.hpp ep[]): the elements per thread change from pass to
@@ -478,17 +433,10 @@ __device__ __forceinline__ void rz_pair(V (&v)[1][EM], int t, const Tw& tw0, con
     }
 }
 
-// the plan's twiddle table into LDS (TW_LDS; every thread of the workgroup calls it)
-template <int K, int P, int THREADS, class Tw>
-__device__ __forceinline__ void tw_setup(Tw& tw, TwPod<CplxOf<P>>* lds_tw, const void* table) {
-    if constexpr (kTwMode<P> == TW_LDS) {
-        const TwPod<CplxOf<P>>* g = static_cast<const TwPod<CplxOf<P>>*>(table);
-        for (int i = threadIdx.x; i < kTwSlots<K, P>; i += THREADS) lds_tw[i] = g[i];
-        __syncthreads();
-        tw.table = (typename Tw::LdsPtr)lds_tw;
-    } else {
-        tw.table = (typename Tw::GlobalPtr)table;
-    }
+// the plan's twiddle table (global; every pass reads its entries where used)
+template <class Tw>
+__device__ __forceinline__ void tw_setup(Tw& tw, const void* table) {
+    tw.table = (typename Tw::GlobalPtr)table;
 }
 
 template <int K, int LAY>
@@ -514,7 +462,7 @@ struct ColGeo {
     static constexpr bool WAVE = THREADS <= 64;
     static constexpr int SLOTS = lds_line(PlanOf<K>::N) * CW;
     static constexpr bool kValid = THREADS >= 64 && THREADS <= 1024 &&
-                                   (SLOTS + kTwSlots<K, P>) * (int)sizeof(CplxOf<P>) <= 160 * 1024;
+                                   SLOTS * (int)sizeof(CplxOf<P>) <= 160 * 1024;
 };
 
 template <int K, int OP, int LAY, int P>
@@ -536,7 +484,6 @@ __global__ void __launch_bounds__((RowGeo<K, LAY>::THREADS), (RowGeo<K, LAY>::MI
     using LD = MxEnd<K, INV_FIRST, true>;
     using ST = MxEnd<K, INV_LAST, false>;
     __shared__ C smem[RPW * LINE];
-    __shared__ TwPod<C> lds_tw[kTwSlots<K, P>];
     // lane -> (row of the tile, t); LAY_B2 pairs: lanes 4k .. 4k + 3 = (r, 2k), (r, 2k + 1),
     // (r + 1, 2k), (r + 1, 2k + 1) -- one 64-B piece of a panel per four lanes and slot
     int t, lrow;
@@ -596,10 +543,7 @@ __global__ void __launch_bounds__((RowGeo<K, LAY>::THREADS), (RowGeo<K, LAY>::MI
             }
         }
     }
-    // the LDS twiddle copy behind the line's loads: its global loads and the
-    // line's are in flight together (a 1080-point complex64 column tile copies
-    // 17 KB of both pass orders)
-    tw_setup<K, P, RowGeo<K, LAY>::THREADS>(tw, lds_tw, a.pl.tw);
+    tw_setup(tw, a.pl.tw);
     if constexpr (OP == RO_FWD || OP == RO_WARM || OP == RO_GD_INIT) {
         rz_line<K, false, C>(v, t, tw, lds);
     } else if constexpr (OP == RO_INV) {
@@ -682,7 +626,6 @@ __global__ void __launch_bounds__((ColGeo<K, CW, P>::THREADS), 1) rz_col_kernel(
     using LD = MxEnd<K, INV_FIRST, true>;
     using ST = MxEnd<K, INV_LAST, false>;
     __shared__ C smem[ColGeo<K, CW, P>::SLOTS];
-    __shared__ TwPod<C> lds_tw[kTwSlots<K, P>];
     const int c = threadIdx.x % CW, t = threadIdx.x / CW;
     const int id = xcd_remap(blockIdx.x, gridDim.x);  // neighbouring tiles (partial lines) on one XCD
     const int b = id / a.nwg;
@@ -714,7 +657,7 @@ __global__ void __launch_bounds__((ColGeo<K, CW, P>::THREADS), 1) rz_col_kernel(
                 v[0][m] = in[st_at(p)];
         }
     }
-    tw_setup<K, P, THREADS>(tw, lds_tw, a.pl.tw);  // behind the line's loads (rz_row_kernel)
+    tw_setup(tw, a.pl.tw);
     if constexpr (OP == CO_FWD) {
         rz_line<K, false, C>(v, t, tw, lds);
     } else if constexpr (OP == CO_INV || OP == CO_AMP_INV) {
