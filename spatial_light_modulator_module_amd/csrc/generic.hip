@@ -657,16 +657,18 @@ int mr_roots(hipStream_t st) {
 // two-column tiles at <= 128 VGPRs, 16 waves per CU where the E = 16 tiles
 // hold 8); $SLM_RZ_PLAN / $SLM_RZ_ROW_PLAN / $SLM_RZ_COL_PLAN =
 // wide|narrow|e8 force a variant (per axis for the last two).
-int rz_key(int n, long long elems, bool col, int prec) {
+int rz_key(int n, long long elems, bool col, int prec, int algo) {
     const int wide = plan_index(n, 0), narrow = plan_index(n, 1), e8 = plan_index(n, 2), panel = plan_index(n, 3);
     if (rz::key_built(panel, prec)) {
         // variant 4 (1920 = 8.16.15 on 240 threads) for rows, where it measured
-        // faster (1080 x 1920 row pass 30.1 -> 25.3 us), variant 3 for columns
-        // (1920 x 1080 column pass 36.0 against 39.8, profiles/r06/speed_c64_alt_q.txt);
+        // faster (complex64 GS 1080 x 1920 row pass 30.1 -> 25.3 us, complex128 GD
+        // 52.3 -> 43.9), variant 3 (15.16.8, 128 threads) for columns (1920 x 1080
+        // column pass 36.0 against 39.8, profiles/r06/speed_c64_alt_q.txt) and for
+        // complex128 GS rows (34.6 -> 29.0 us, profiles/r06/ab_rows_f64_zh.txt);
         // $SLM_RZ_PANEL=alt|main forces one
         const int alt = plan_index(n, 4);
         const char* a = std::getenv("SLM_RZ_PANEL");
-        const bool use_alt = a ? !std::strcmp(a, "alt") : !col;
+        const bool use_alt = a ? !std::strcmp(a, "alt") : !col && !(prec == PREC_F64 && algo == SLM_ALGO_GS);
         return use_alt && rz::key_built(alt, prec) ? alt : panel;
     }
     const bool w_ok = rz::key_built(wide, prec), n_ok = rz::key_built(narrow, prec), e_ok = rz::key_built(e8, prec);
@@ -723,8 +725,8 @@ bool rz_shape(int B, int H, int W, RzChoice* c, int algo, int prec) {
     if (e && (!std::strcmp(e, "mr") || !std::strcmp(e, "gemm") || !std::strcmp(e, "bluestein"))) return false;
     if (prec == PREC_F32 && algo != SLM_ALGO_GS) return false;
     const long long elems = (long long)B * H * W;
-    c->rkey = rz_key(W, elems, false, prec);
-    c->ckey = rz_key(H, elems, true, prec);
+    c->rkey = rz_key(W, elems, false, prec, algo);
+    c->ckey = rz_key(H, elems, true, prec, algo);
     if (c->rkey < 0 || c->ckey < 0) return false;
     c->cw = rz_cw_of(c->ckey, W, prec);
     c->lay = rz_layout(algo, H, W, prec);
