@@ -465,8 +465,16 @@ struct ColGeo {
                                    SLOTS * (int)sizeof(CplxOf<P>) <= 160 * 1024;
 };
 
+// waves-per-SIMD floor of a row kernel: RowGeo's, and for the complex64 rows of
+// the 240-thread 1920 plan (480-thread row-pair tiles, 8 waves) 6 per SIMD --
+// three tiles per CU, so a 1080-row panel's 540 tiles run in one round
+template <int K, int LAY, int P>
+constexpr int row_min_waves() {
+    return (P == PREC_F32 && RowGeo<K, LAY>::THREADS == 480) ? 6 : RowGeo<K, LAY>::MIN_WAVES;
+}
+
 template <int K, int OP, int LAY, int P>
-__global__ void __launch_bounds__((RowGeo<K, LAY>::THREADS), (RowGeo<K, LAY>::MIN_WAVES)) rz_row_kernel(mr::RowArgs a) {
+__global__ void __launch_bounds__((RowGeo<K, LAY>::THREADS), (row_min_waves<K, LAY, P>())) rz_row_kernel(mr::RowArgs a) {
     using C = CplxOf<P>;  // compute and state type
     using S = Scalar<C>;
     using namespace mr;
