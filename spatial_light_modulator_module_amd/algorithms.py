@@ -24,8 +24,8 @@ Engines and the cost model (see DESIGN.md sections 1, 3 and 5):
 * 13-smooth SLM panel sides (600, 800, 1000, 1080, 1152, 1200, 1280, 1536,
   1920, and 2^k / 768 on the other axis): the radix kernels on mixed-E
   Stockham plans -- float32 GS targets in complex64 with the float32 engine's
-  numerics (GS 1080 x 1920: ~0.048 ms per iteration), uint8 GS, GD and
-  float64 runs in complex128 (GS ~0.070, GD ~0.088 ms);
+  numerics (GS 1080 x 1920: ~0.043 ms per iteration), uint8 GS, GD and
+  float64 runs in complex128 (GS ~0.061, GD ~0.082 ms);
 * any other shape whose sides factor into 2, 3, 5, 7, 11, 13: the float64
   mixed-radix kernels, complex128 state, two launches per iteration (~0.08 ms
   per iteration at 2 Mpixel);
